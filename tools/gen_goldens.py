@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ by running the REAL reference.
+
+Runs only in the build container (where /root/reference exists).  It imports the
+reference's own `models/pose_loss.py` and `models/add_loss.py` (both import as-is:
+they need only torch/numpy/yaml) and records their outputs on seeded synthetic
+inputs.  Nothing from the reference is copied: the fixtures are inputs + outputs.
+
+    python tools/gen_goldens.py            # rewrites tests/golden/*.npz
+
+The reference's `models/pose_net_*.py` need torchvision, which is absent from this
+image; no stand-in is written for it, so model-forward parity is anchored on the
+build's CPU restatement (oracle/resnet.py) -- see DESIGN.md "Oracle".
+"""
+import importlib.util
+import json
+import os
+import sys
+import tempfile
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, REPO)
+from tests.synth import write_mesh_dir, LINEMOD_OBJ_IDS, make_poses, grid_mesh  # noqa: E402
+
+REF = os.environ.get("POSE6D_REFERENCE", "/root/reference")
+OUT = os.path.join(REPO, "tests", "golden")
+
+
+def _load(modname, relpath):
+    spec = importlib.util.spec_from_file_location(modname, os.path.join(REF, relpath))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def gen_pose_loss(ref_pl):
+    g = torch.Generator().manual_seed(7)
+    cases = {}
+    B = 32
+    gt = torch.nn.functional.normalize(torch.randn(B, 4, generator=g), dim=1)
+    cases["random"] = (torch.randn(B, 4, generator=g), torch.randn(B, 3, generator=g) * 0.1 + torch.tensor([0, 0, .8]),
+                       gt, torch.randn(B, 3, generator=g) * 0.1 + torch.tensor([0, 0, .8]))
+    gt8 = torch.nn.functional.normalize(torch.randn(8, 4, generator=g), dim=1)
+    t8 = torch.randn(8, 3, generator=g)
+    cases["identical"] = (gt8.clone(), t8.clone(), gt8.clone(), t8.clone())
+    cases["antipodal"] = (-gt8.clone() * 3.0, t8 + 0.01, gt8.clone(), t8.clone())
+    zr = torch.randn(8, 4, generator=g)
+    zr[2] = 0.0
+    zr[5] = 1e-20
+    cases["zero_norm"] = (zr, t8 * 2, gt8.clone(), t8.clone())
+    # orthogonal quaternions: dot == 0 exactly (q2 = [-y, x, -w, z])
+    q = gt8.clone()
+    orth = torch.stack([-q[:, 1], q[:, 0], -q[:, 3], q[:, 2]], dim=1)
+    cases["orthogonal"] = (orth, t8, q, t8 + 0.5)
+    cases["single"] = (torch.randn(1, 4, generator=g), torch.randn(1, 3, generator=g), gt8[:1].clone(), t8[:1].clone())
+    cases["scaled"] = (gt8 * 1e3 + 1e-3 * torch.randn(8, 4, generator=g), t8, gt8, t8 - 0.25)
+
+    out = {}
+    modes = [("geodesic", 1.0, 10.0), ("geodesic", 1.0, 1.0), ("l1", 1.0, 10.0), ("l1", 0.5, 2.0)]
+    for name, (pr, pt, gr, gtt) in cases.items():
+        out[f"{name}/pred_rot"] = pr.numpy()
+        out[f"{name}/pred_trans"] = pt.numpy()
+        out[f"{name}/gt_rot"] = gr.numpy()
+        out[f"{name}/gt_trans"] = gtt.numpy()
+        for mode, wr, wt in modes:
+            crit = ref_pl.PoseLoss(rot_weight=wr, trans_weight=wt, rotation_loss=mode)
+            a = pr.clone().requires_grad_(True)
+            b = pt.clone().requires_grad_(True)
+            loss = crit(a, b, gr, gtt)
+            loss.backward()
+            key = f"{name}/{mode}_{wr:g}_{wt:g}"
+            out[key + "/loss"] = np.asarray(loss.detach().numpy(), dtype=np.float32)
+            out[key + "/grad_rot"] = a.grad.numpy()
+            out[key + "/grad_trans"] = b.grad.numpy()
+    np.savez_compressed(os.path.join(OUT, "pose_loss.npz"), **out)
+    meta = {"cases": list(cases), "modes": [f"{m}_{a:g}_{b:g}" for m, a, b in modes]}
+    with open(os.path.join(OUT, "pose_loss.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+
+
+def _per_point(crit, pred_r, pred_t, gt_r, gt_t, obj_ids):
+    """Per-sample ADD / ADD-S, per-point min distance and argmin, following the
+    op sequence of add_loss.py:161-189 on the reference's own matrices."""
+    pR = crit._quat_to_mat(pred_r)
+    gR = crit._quat_to_mat(gt_r)
+    add, adds, mins, idxs, valid = [], [], [], [], []
+    for i in range(pred_r.shape[0]):
+        oid = int(obj_ids[i].item())
+        if oid not in crit.points:
+            valid.append(0)
+            continue
+        valid.append(1)
+        P = crit.points[oid]
+        G = torch.mm(P, gR[i].T) + gt_t[i]
+        Q = torch.mm(P, pR[i].T) + pred_t[i]
+        add.append(torch.norm(Q - G, dim=1, p=2).mean().item())
+        d = torch.norm(Q.unsqueeze(1) - G.unsqueeze(0), dim=2)
+        v, j = d.min(dim=1)
+        adds.append(v.mean().item())
+        mins.append(v.numpy())
+        idxs.append(j.numpy().astype(np.int32))
+    return (np.asarray(add, np.float64), np.asarray(adds, np.float64), mins, idxs,
+            np.asarray(valid, np.int32), pR.numpy(), gR.numpy())
+
+
+def gen_add(ref_al):
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        write_mesh_dir(d, n_vertices=700, seed=11)
+        np.random.seed(1234)
+        crit = ref_al.ADDLoss(d, "cpu")
+        # loader results (seeded global np.random, add_loss.py:68,78)
+        for oid in sorted(crit.points):
+            out[f"load/points/{oid}"] = crit.points[oid].numpy()
+        out["load/diam_ids"] = np.asarray(sorted(crit.diameters), np.int32)
+        out["load/diam_vals"] = np.asarray([crit.diameters[k] for k in sorted(crit.diameters)], np.float64)
+
+        # --- N = 500 (reference default), B = 64 incl. unknown ids ------------
+        rng = np.random.default_rng(5)
+        ids = np.array([LINEMOD_OBJ_IDS[i % 13] for i in range(60)] + [2, 6, 20, 9], np.int64)
+        pr, pt, gr, gt = make_poses(rng, len(ids))
+        args = [torch.from_numpy(x) for x in (pr, pt, gr, gt)] + [torch.from_numpy(ids)]
+        m = crit.eval_metrics(*args)
+        out["n500/pred_rot"], out["n500/pred_trans"], out["n500/gt_rot"], out["n500/gt_trans"] = pr, pt, gr, gt
+        out["n500/obj_ids"] = ids
+        out["n500/metrics"] = np.asarray([m["add_mean"], m["add_s_mean"], m["add_01d_acc"]], np.float64)
+        out["n500/forward"] = np.asarray(crit(*args).item(), np.float64)
+        add, adds, mins, idxs, valid, pR, gR = _per_point(crit, *args)
+        out["n500/add"], out["n500/adds"], out["n500/valid"] = add, adds, valid
+        out["n500/pred_R"], out["n500/gt_R"] = pR, gR
+        out["n500/min_dist"] = np.concatenate(mins)
+        out["n500/npts"] = np.asarray([len(x) for x in mins], np.int32)
+        out["n500/argmin"] = np.concatenate(idxs)
+
+        # --- N = 2000 (BASELINE config 4 size): override the points dict -----
+        rng = np.random.default_rng(6)
+        for oid in LINEMOD_OBJ_IDS:
+            crit.points[oid] = torch.from_numpy((rng.standard_normal((2000, 3)) * 0.04).astype(np.float32))
+        ids = np.array([LINEMOD_OBJ_IDS[i % 13] for i in range(26)], np.int64)
+        pr, pt, gr, gt = make_poses(rng, len(ids))
+        args = [torch.from_numpy(x) for x in (pr, pt, gr, gt)] + [torch.from_numpy(ids)]
+        m = crit.eval_metrics(*args)
+        for oid in LINEMOD_OBJ_IDS:
+            out[f"n2000/points/{oid}"] = crit.points[oid].numpy()
+        out["n2000/pred_rot"], out["n2000/pred_trans"], out["n2000/gt_rot"], out["n2000/gt_trans"] = pr, pt, gr, gt
+        out["n2000/obj_ids"] = ids
+        out["n2000/metrics"] = np.asarray([m["add_mean"], m["add_s_mean"], m["add_01d_acc"]], np.float64)
+        out["n2000/forward"] = np.asarray(crit(*args).item(), np.float64)
+        add, adds, mins, idxs, valid, _, _ = _per_point(crit, *args)
+        out["n2000/add"], out["n2000/adds"], out["n2000/valid"] = add, adds, valid
+        out["n2000/min_dist"] = np.concatenate(mins)
+        out["n2000/npts"] = np.asarray([len(x) for x in mins], np.int32)
+        out["n2000/argmin"] = np.concatenate(idxs)
+
+        # --- ties: integer-mm grid meshes with duplicated vertices ---------------
+        rng = np.random.default_rng(8)
+        for oid in LINEMOD_OBJ_IDS:
+            crit.points[oid] = torch.from_numpy(grid_mesh(rng, 600))
+        ids = np.array(LINEMOD_OBJ_IDS, np.int64)
+        pr, pt, gr, gt = make_poses(rng, len(ids))
+        # exact identity pose for a few samples: every point has distance-0 ties
+        pr[:3], pt[:3] = gr[:3], gt[:3]
+        pr[3] = -gr[3]  # antipodal quaternion: the same rotation
+        pt[3] = gt[3]
+        args = [torch.from_numpy(x) for x in (pr, pt, gr, gt)] + [torch.from_numpy(ids)]
+        m = crit.eval_metrics(*args)
+        for oid in LINEMOD_OBJ_IDS:
+            out[f"ties/points/{oid}"] = crit.points[oid].numpy()
+        out["ties/pred_rot"], out["ties/pred_trans"], out["ties/gt_rot"], out["ties/gt_trans"] = pr, pt, gr, gt
+        out["ties/obj_ids"] = ids
+        out["ties/metrics"] = np.asarray([m["add_mean"], m["add_s_mean"], m["add_01d_acc"]], np.float64)
+        add, adds, mins, idxs, valid, _, _ = _per_point(crit, *args)
+        out["ties/add"], out["ties/adds"], out["ties/valid"] = add, adds, valid
+        out["ties/min_dist"] = np.concatenate(mins)
+        out["ties/npts"] = np.asarray([len(x) for x in mins], np.int32)
+        out["ties/argmin"] = np.concatenate(idxs)
+
+        # --- empty batch / all-unknown ids ---------------------------------------
+        args = [torch.zeros(0, 4), torch.zeros(0, 3), torch.zeros(0, 4), torch.zeros(0, 3), torch.zeros(0, dtype=torch.long)]
+        m = crit.eval_metrics(*args)
+        out["empty/metrics"] = np.asarray([m["add_mean"], m["add_s_mean"], m["add_01d_acc"]], np.float64)
+        args = [torch.ones(2, 4), torch.ones(2, 3), torch.ones(2, 4), torch.ones(2, 3), torch.tensor([2, 99])]
+        m = crit.eval_metrics(*args)
+        out["unknown/metrics"] = np.asarray([m["add_mean"], m["add_s_mean"], m["add_01d_acc"]], np.float64)
+        out["unknown/forward"] = np.asarray(crit(*args).item(), np.float64)
+    out["symmetric_ids"] = np.asarray(sorted(ref_al.SYMMETRIC_OBJECT_IDS), np.int32)
+    np.savez_compressed(os.path.join(OUT, "add_loss.npz"), **out)
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    torch.set_num_threads(1)
+    ref_pl = _load("ref_pose_loss", "models/pose_loss.py")
+    ref_al = _load("ref_add_loss", "models/add_loss.py")
+    gen_pose_loss(ref_pl)
+    gen_add(ref_al)
+    for f in sorted(os.listdir(OUT)):
+        print(f, os.path.getsize(os.path.join(OUT, f)))
+
+
+if __name__ == "__main__":
+    main()
