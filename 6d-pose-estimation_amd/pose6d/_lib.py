@@ -1,0 +1,102 @@
+"""ctypes binding of libpose6d.so (the C ABI declared in include/pose6d.h).
+
+The library is the product: there is no CPU or eager-PyTorch fallback.  Loading
+fails loudly if the .so is missing, and every op raises if handed a tensor that
+is not on a ROCm device.
+"""
+import ctypes
+import os
+import re
+
+import torch  # noqa: F401  (loads torch's HIP runtime first; libpose6d binds to the same libamdhip64.so.7)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libpose6d.so")
+HEADER = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "pose6d.h")
+
+DT_F32 = 0
+DT_BF16 = 1
+
+_lib = None
+
+
+class Pose6dError(RuntimeError):
+    pass
+
+
+_CT = {
+    "int": ctypes.c_int, "int32_t": ctypes.c_int32, "int64_t": ctypes.c_int64, "float": ctypes.c_float,
+    "double": ctypes.c_double, "void": None, "char": ctypes.c_char,
+}
+
+
+def _parse_header(path):
+    """Parse `int pose6d_xxx(args);` prototypes -> {name: [ctypes argtypes]}."""
+    src = open(path).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    protos = {}
+    for m in re.finditer(r"\b(int|const char\s*\*)\s*(pose6d_\w+)\s*\(([^)]*)\)\s*;", src):
+        name, args = m.group(2), m.group(3).strip()
+        types = []
+        if args and args != "void":
+            for a in args.split(","):
+                a = a.strip()
+                if "*" in a:
+                    types.append(ctypes.c_void_p)
+                else:
+                    base = a.replace("const", "").split()[0]
+                    types.append(_CT[base])
+        protos[name] = (types, m.group(1).startswith("const"))
+    return protos
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise Pose6dError(f"libpose6d.so not built ({LIB_PATH}); run `python -c 'import __graft_entry__ as g; g.build()'`"
+                          " or `make -C 6d-pose-estimation_amd/csrc`")
+    lib = ctypes.CDLL(LIB_PATH)
+    protos = _parse_header(HEADER) if os.path.exists(HEADER) else {}
+    for name, (argtypes, ret_str) in protos.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_char_p if ret_str else ctypes.c_int
+    lib._protos = protos
+    _lib = lib
+    return lib
+
+
+def symbols():
+    load()
+    return sorted(_lib._protos)
+
+
+def call(name, *args):
+    """Call pose6d_<name>; tensors are passed as data pointers; raise on error."""
+    lib = load()
+    fn = getattr(lib, "pose6d_" + name)
+    conv = []
+    for a in args:
+        if isinstance(a, torch.Tensor):
+            conv.append(ctypes.c_void_p(a.data_ptr()))
+        elif a is None:
+            conv.append(None)
+        else:
+            conv.append(a)
+    rc = fn(*conv)
+    if rc != 0:
+        raise Pose6dError(f"pose6d_{name} failed ({rc}): {lib.pose6d_last_error().decode()}")
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is not None and isinstance(t, torch.Tensor) and not t.is_cuda:
+            raise Pose6dError("pose6d ops run only on a ROCm device (MI355X); got a CPU tensor. "
+                              "There is no CPU fallback by design.")

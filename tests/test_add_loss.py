@@ -1,0 +1,105 @@
+"""ADDLoss drop-in: host loader (CPU) and the HIP evaluator (GPU) against the
+golden vectors produced by the reference's own add_loss.py."""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+from tests.synth import LINEMOD_OBJ_IDS, make_poses, synthetic_meshes, write_mesh_dir
+
+
+def _make(device):
+    from models.add_loss import ADDLoss
+    d = tempfile.mkdtemp()
+    write_mesh_dir(d, n_vertices=700, seed=11)
+    np.random.seed(1234)
+    return ADDLoss(d, device)
+
+
+def test_loader_bit_exact_vs_reference(golden):
+    g = golden["add_loss"]
+    crit = _make("cpu")
+    ref = {o: g[f"load/points/{o}"] for o in LINEMOD_OBJ_IDS if f"load/points/{o}" in g}
+    assert sorted(crit.points) == sorted(ref)
+    for o in ref:
+        assert crit.points[o].numpy().tobytes() == ref[o].tobytes()
+    np.testing.assert_array_equal([crit.diameters[k] for k in sorted(crit.diameters)], g["load/diam_vals"])
+
+
+def _args(g, tag, dev):
+    return [torch.from_numpy(g[f"{tag}/{k}"]).to(dev) for k in ("pred_rot", "pred_trans", "gt_rot", "gt_trans",
+                                                               "obj_ids")]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", ["n500", "n2000", "ties"])
+def test_add_eval_gpu_vs_reference(golden, tag):
+    g = golden["add_loss"]
+    crit = _make("cuda")
+    if tag != "n500":
+        for o in LINEMOD_OBJ_IDS:
+            crit.points[o] = torch.from_numpy(g[f"{tag}/points/{o}"]).cuda()
+    args = _args(g, tag, "cuda")
+    s = crit.per_sample(*args, want_points=True)
+    valid = s["valid"].cpu().numpy()
+    np.testing.assert_array_equal(valid, g[f"{tag}/valid"])
+    npts = g[f"{tag}/npts"]
+    mins, amins = s["min"].cpu().numpy(), s["argmin"].cpu().numpy()
+    vi = np.nonzero(valid)[0]
+    got_min = np.concatenate([mins[b, :n] for b, n in zip(vi, npts)])
+    got_arg = np.concatenate([amins[b, :n] for b, n in zip(vi, npts)])
+    assert got_min.tobytes() == g[f"{tag}/min_dist"].tobytes(), "per-point ADD-S min distance not bit-exact"
+    np.testing.assert_array_equal(got_arg, g[f"{tag}/argmin"])          # bit-exact argmin
+    np.testing.assert_allclose(s["add"].cpu().numpy()[vi], g[f"{tag}/add"], rtol=1e-6)
+    np.testing.assert_allclose(s["adds"].cpu().numpy()[vi], g[f"{tag}/adds"], rtol=1e-6)
+    m = crit.eval_metrics(*args)
+    np.testing.assert_allclose([m["add_mean"], m["add_s_mean"], m["add_01d_acc"]], g[f"{tag}/metrics"], rtol=1e-6)
+    if f"{tag}/forward" in g:
+        np.testing.assert_allclose(crit(*args).item(), g[f"{tag}/forward"], rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_add_eval_gpu_edges(golden):
+    g = golden["add_loss"]
+    crit = _make("cuda")
+    e = torch.zeros(0, 4, device="cuda")
+    m = crit.eval_metrics(e, e[:, :3], e, e[:, :3], torch.zeros(0, dtype=torch.long, device="cuda"))
+    np.testing.assert_array_equal([m["add_mean"], m["add_s_mean"], m["add_01d_acc"]], g["empty/metrics"])
+    o = torch.ones(2, 4, device="cuda")
+    args = [o, o[:, :3], o, o[:, :3], torch.tensor([2, 99], device="cuda")]
+    m = crit.eval_metrics(*args)
+    np.testing.assert_array_equal([m["add_mean"], m["add_s_mean"], m["add_01d_acc"]], g["unknown/metrics"])
+    assert crit(*args).item() == g["unknown/forward"]
+
+
+@pytest.mark.gpu
+def test_add_eval_c4_full_size_vs_oracle():
+    """BASELINE config 4 shape: B=256 x 2000 points x 13 objects; every sample's
+    argmin vs the C oracle on a 24-sample subset, plus size-independent checks."""
+    from models.add_loss import ADDLoss
+    from oracle import add_loss as OA
+    pts, diam = synthetic_meshes(2000, seed=0)
+    crit = ADDLoss.__new__(ADDLoss)
+    torch.nn.Module.__init__(crit)
+    crit.points = {k: torch.from_numpy(v).cuda() for k, v in pts.items()}
+    crit.diameters, crit.device, crit._table = diam, "cuda", None
+    rng = np.random.default_rng(3)
+    ids = np.array([LINEMOD_OBJ_IDS[i % 13] for i in range(256)], np.int64)
+    pr, pt, gr, gt = make_poses(rng, 256)
+    args = [torch.from_numpy(x).cuda() for x in (pr, pt, gr, gt, ids)]
+    s = crit.per_sample(*args, want_points=True)
+    mins, amin = s["min"].cpu().numpy(), s["argmin"].cpu().numpy()
+    for b in range(0, 256, 11):
+        P = pts[int(ids[b])]
+        G = OA.transform(P, OA.quat_to_mat(gr[b:b + 1])[0], gt[b])
+        Q = OA.transform(P, OA.quat_to_mat(pr[b:b + 1])[0], pt[b])
+        m, j = OA.adds_min(Q, G)
+        assert mins[b].tobytes() == m.tobytes()
+        np.testing.assert_array_equal(amin[b], j)
+    # identity pose: every point's nearest gt point is itself at distance 0
+    args2 = [args[2], args[3], args[2], args[3], args[4]]
+    s2 = crit.per_sample(*args2, want_points=True)
+    assert float(s2["min"].abs().max()) == 0.0
+    assert float(s2["adds"].abs().max()) == 0.0
