@@ -1,0 +1,323 @@
+// BatchNorm2d (train/eval) + ReLU + residual for NHWC activations, forward and
+// backward.  Replaces the nn.BatchNorm2d / ReLU / residual-add chain of every
+// torchvision Bottleneck (53 BN layers per ResNet50 trunk).
+//
+// Forward statistics come from the producing convolution's epilogue (per-wave
+// partial sums in a [rows][2][C] workspace); pose6d_bn_finalize reduces them in
+// fixed order (fp64), produces per-channel scale/shift, the saved mean/invstd and
+// the running-stat update (torch semantics: biased var to normalise, unbiased var
+// into running_var, momentum 0.1, num_batches_tracked += 1).
+// pose6d_bn_act_fwd then applies  out = act(y*scale + shift [+ res | + res*rs + rsh]).
+// Backward: pose6d_bn_bwd_reduce -> partial (sum dz, sum dz*xhat) per block,
+// pose6d_bn_bwd_finalize -> dgamma/dbeta + coefficients, pose6d_bn_bwd_apply ->
+// dy = gamma*invstd*(dz - mean(dz) - xhat*mean(dz*xhat)), optionally emitting dz
+// (the gradient of a residual identity branch).
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+template <typename T> struct V;
+template <> struct V<bf16> { static constexpr int E = 8; };
+template <> struct V<float> { static constexpr int E = 4; };
+
+template <typename T>
+__device__ __forceinline__ void load_vec(const T* p, float* f) {
+  constexpr int E = V<T>::E;
+  T t[E];
+  *reinterpret_cast<uint4*>(t) = *reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int e = 0; e < E; ++e) f[e] = p6::to_f(t[e]);
+}
+template <typename T>
+__device__ __forceinline__ void store_vec(T* p, const float* f) {
+  constexpr int E = V<T>::E;
+  T t[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) t[e] = p6::from_f<T>(f[e]);
+  *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(t);
+}
+
+// ---------------------------------------------------------------- finalize
+__global__ __launch_bounds__(kThreads) void bn_finalize_kernel(
+    const float* __restrict__ part, int rows, int C, double count, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
+    float momentum, float eps, int training, float* __restrict__ scale, float* __restrict__ shift,
+    float* __restrict__ smean, float* __restrict__ sinv) {
+  __shared__ double red[2][4][64];
+  const int cl = threadIdx.x & 63, pr = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  if (training) {
+    double s = 0.0, q = 0.0;
+    if (c < C)
+      for (int r = pr; r < rows; r += 4) {
+        s += (double)part[(int64_t)r * 2 * C + c];
+        q += (double)part[(int64_t)r * 2 * C + C + c];
+      }
+    red[0][pr][cl] = s;
+    red[1][pr][cl] = q;
+    __syncthreads();
+    if (pr == 0 && c < C) {
+      s = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+      q = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+      const double mean = s / count;
+      double var = q / count - mean * mean;
+      if (var < 0.0) var = 0.0;
+      const float inv = (float)(1.0 / sqrt(var + (double)eps));
+      const float sc = gamma[c] * inv;
+      scale[c] = sc;
+      shift[c] = beta[c] - (float)mean * sc;
+      smean[c] = (float)mean;
+      sinv[c] = inv;
+      const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) nbt[0] += 1;
+  } else if (pr == 0 && c < C) {
+    const float inv = 1.0f / sqrtf(rvar[c] + eps);
+    const float sc = gamma[c] * inv;
+    scale[c] = sc;
+    shift[c] = beta[c] - rmean[c] * sc;
+    smean[c] = rmean[c];
+    sinv[c] = inv;
+  }
+}
+
+// ---------------------------------------------------------------- apply fwd
+template <typename T>
+__global__ __launch_bounds__(kThreads) void bn_act_kernel(const T* __restrict__ y, const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, const T* __restrict__ res,
+                                                          const float* __restrict__ rscale,
+                                                          const float* __restrict__ rshift, int relu,
+                                                          T* __restrict__ out, int64_t M, int C) {
+  constexpr int E = V<T>::E;
+  const int cpr = C / E;
+  const int64_t total = M * cpr;
+  for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < total; i += (int64_t)gridDim.x * kThreads) {
+    const int c0 = (int)(i % cpr) * E;
+    const int64_t off = i * E;
+    float v[E], r[E];
+    load_vec(y + off, v);
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] = fmaf(v[e], scale[c0 + e], shift[c0 + e]);
+    if (res) {
+      load_vec(res + off, r);
+      if (rscale) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] += fmaf(r[e], rscale[c0 + e], rshift[c0 + e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] += r[e];
+      }
+    }
+    if (relu) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    store_vec(out + off, v);
+  }
+}
+
+// ---------------------------------------------------------------- backward
+// Each block: ROWS_PER_BLOCK rows x all channels; thread = (row lane, channel chunk).
+template <typename T>
+__global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __restrict__ dout, const T* __restrict__ out,
+                                                                 const T* __restrict__ y, const float* __restrict__ mean,
+                                                                 const float* __restrict__ inv, float* __restrict__ part,
+                                                                 int64_t M, int C, int rows_per_block) {
+  constexpr int E = V<T>::E;
+  extern __shared__ float sred[];  // [kThreads][2*E]
+  const int cpr = C / E;
+  const int tpr = kThreads / cpr > 0 ? kThreads / cpr : 1;  // threads along rows
+  const int cc = threadIdx.x % cpr, rl = threadIdx.x / cpr;
+  float s[E], q[E];
+  // channel chunks beyond kThreads are looped (then tpr == 1: no cross-thread reduce)
+  for (int ch = cc; ch < cpr; ch += kThreads) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) s[e] = q[e] = 0.f;
+    const int c0 = ch * E;
+    float mu[E], iv[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) { mu[e] = mean[c0 + e]; iv[e] = inv[c0 + e]; }
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = min(M, r0 + rows_per_block);
+    if (rl < tpr)
+      for (int64_t r = r0 + rl; r < r1; r += tpr) {
+        const int64_t off = r * C + c0;
+        float d[E], yy[E];
+        load_vec(dout + off, d);
+        if (out) {
+          float o[E];
+          load_vec(out + off, o);
+#pragma unroll
+          for (int e = 0; e < E; ++e) d[e] = o[e] > 0.f ? d[e] : 0.f;
+        }
+        load_vec(y + off, yy);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          s[e] += d[e];
+          q[e] = fmaf(d[e], (yy[e] - mu[e]) * iv[e], q[e]);
+        }
+      }
+    // reduce over the tpr row-threads sharing this chunk
+    if (cpr <= kThreads) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) { sred[threadIdx.x * 2 * E + e] = s[e]; sred[threadIdx.x * 2 * E + E + e] = q[e]; }
+      __syncthreads();
+      if (rl == 0) {
+        for (int k = 1; k < tpr; ++k) {
+          const int t = k * cpr + cc;
+#pragma unroll
+          for (int e = 0; e < E; ++e) { s[e] += sred[t * 2 * E + e]; q[e] += sred[t * 2 * E + E + e]; }
+        }
+        float* pp = part + (int64_t)blockIdx.x * 2 * C;
+#pragma unroll
+        for (int e = 0; e < E; ++e) { pp[c0 + e] = s[e]; pp[C + c0 + e] = q[e]; }
+      }
+      __syncthreads();
+    } else {
+      float* pp = part + (int64_t)blockIdx.x * 2 * C;
+#pragma unroll
+      for (int e = 0; e < E; ++e) { pp[c0 + e] = s[e]; pp[C + c0 + e] = q[e]; }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void bn_bwd_finalize_kernel(const float* __restrict__ part, int rows, int C,
+                                                                   double count, const float* __restrict__ gamma,
+                                                                   const float* __restrict__ inv,
+                                                                   float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                                   int accumulate, float* __restrict__ coef) {
+  __shared__ double red[2][4][64];
+  const int cl = threadIdx.x & 63, pr = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double s = 0.0, q = 0.0;
+  if (c < C)
+    for (int r = pr; r < rows; r += 4) {
+      s += (double)part[(int64_t)r * 2 * C + c];
+      q += (double)part[(int64_t)r * 2 * C + C + c];
+    }
+  red[0][pr][cl] = s;
+  red[1][pr][cl] = q;
+  __syncthreads();
+  if (pr == 0 && c < C) {
+    s = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+    q = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+    if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)s;
+    if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)q;
+    coef[c] = gamma[c] * inv[c];            // c1
+    coef[C + c] = (float)(s / count);       // c2 = mean(dz)
+    coef[2 * C + c] = (float)(q / count);   // c3 = mean(dz * xhat)
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const T* __restrict__ dout, const T* __restrict__ out,
+                                                                const T* __restrict__ y, const float* __restrict__ mean,
+                                                                const float* __restrict__ inv,
+                                                                const float* __restrict__ coef, T* __restrict__ dy,
+                                                                T* __restrict__ dz_out, int64_t M, int C) {
+  constexpr int E = V<T>::E;
+  const int cpr = C / E;
+  const int64_t total = M * cpr;
+  for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < total; i += (int64_t)gridDim.x * kThreads) {
+    const int c0 = (int)(i % cpr) * E;
+    const int64_t off = i * E;
+    float d[E], yy[E], r[E];
+    load_vec(dout + off, d);
+    if (out) {
+      float o[E];
+      load_vec(out + off, o);
+#pragma unroll
+      for (int e = 0; e < E; ++e) d[e] = o[e] > 0.f ? d[e] : 0.f;
+    }
+    if (dz_out) store_vec(dz_out + off, d);
+    load_vec(y + off, yy);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int c = c0 + e;
+      const float xh = (yy[e] - mean[c]) * inv[c];
+      r[e] = coef[c] * (d[e] - coef[C + c] - xh * coef[2 * C + c]);
+    }
+    store_vec(dy + off, r);
+  }
+}
+
+inline unsigned grid_for(int64_t chunks) {
+  int64_t b = (chunks + kThreads - 1) / kThreads;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+int rows_per_block(int64_t M) {
+  // ~256 blocks of work, at least 64 rows each
+  int64_t r = (M + 255) / 256;
+  if (r < 64) r = 64;
+  return (int)r;
+}
+
+}  // namespace
+
+extern "C" int pose6d_bn_finalize(const float* partial, int32_t rows, int32_t C, int64_t count, const float* gamma,
+                                  const float* beta, float* running_mean, float* running_var, int64_t* num_batches,
+                                  float momentum, float eps, int32_t training, float* scale, float* shift,
+                                  float* save_mean, float* save_invstd, void* stream) {
+  P6_CHECK_ARG(C > 0 && (!training || (rows > 0 && count > 0)), "pose6d_bn_finalize: bad sizes");
+  bn_finalize_kernel<<<p6::ceil_div(C, 64), kThreads, 0, p6::stream_of(stream)>>>(
+      partial, rows, C, (double)count, gamma, beta, running_mean, running_var, num_batches, momentum, eps, training,
+      scale, shift, save_mean, save_invstd);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+extern "C" int pose6d_bn_act_fwd(int32_t dtype, const void* y, const float* scale, const float* shift,
+                                 const void* res, const float* res_scale, const float* res_shift, int32_t relu,
+                                 void* out, int64_t M, int32_t C, void* stream) {
+  P6_CHECK_ARG(C % 8 == 0, "pose6d_bn_act_fwd: C %% 8 != 0");
+  hipStream_t s = p6::stream_of(stream);
+  if (dtype == POSE6D_DT_BF16)
+    bn_act_kernel<bf16><<<grid_for(M * C / 8), kThreads, 0, s>>>((const bf16*)y, scale, shift, (const bf16*)res,
+                                                                   res_scale, res_shift, relu, (bf16*)out, M, C);
+  else
+    bn_act_kernel<float><<<grid_for(M * C / 4), kThreads, 0, s>>>((const float*)y, scale, shift, (const float*)res,
+                                                                    res_scale, res_shift, relu, (float*)out, M, C);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+extern "C" int pose6d_bn_bwd_workspace_rows(int64_t M) { return p6::ceil_div(M, rows_per_block(M)); }
+
+extern "C" int pose6d_bn_bwd(int32_t dtype, const void* dout, const void* out, const void* y, const float* mean,
+                             const float* invstd, const float* gamma, float* dgamma, float* dbeta, int32_t accumulate,
+                             void* dy, void* dz_out, float* workspace, int64_t M, int32_t C, void* stream) {
+  P6_CHECK_ARG(C % 8 == 0 && M > 0, "pose6d_bn_bwd: bad sizes");
+  hipStream_t s = p6::stream_of(stream);
+  const int rpb = rows_per_block(M);
+  const int nb = p6::ceil_div(M, rpb);
+  float* part = workspace;                          // [nb][2][C]
+  float* coef = workspace + (int64_t)nb * 2 * C;    // [3][C]
+  if (dtype == POSE6D_DT_BF16) {
+    bn_bwd_reduce_kernel<bf16><<<nb, kThreads, kThreads * 2 * 8 * 4, s>>>(
+        (const bf16*)dout, (const bf16*)out, (const bf16*)y, mean, invstd, part, M, C, rpb);
+  } else {
+    bn_bwd_reduce_kernel<float><<<nb, kThreads, kThreads * 2 * 4 * 4, s>>>(
+        (const float*)dout, (const float*)out, (const float*)y, mean, invstd, part, M, C, rpb);
+  }
+  P6_LAUNCH_CHECK();
+  bn_bwd_finalize_kernel<<<p6::ceil_div(C, 64), kThreads, 0, s>>>(part, nb, C, (double)M, gamma, invstd, dgamma, dbeta,
+                                                                  accumulate, coef);
+  P6_LAUNCH_CHECK();
+  if (dtype == POSE6D_DT_BF16)
+    bn_bwd_apply_kernel<bf16><<<grid_for(M * C / 8), kThreads, 0, s>>>((const bf16*)dout, (const bf16*)out,
+                                                                         (const bf16*)y, mean, invstd, coef, (bf16*)dy,
+                                                                         (bf16*)dz_out, M, C);
+  else
+    bn_bwd_apply_kernel<float><<<grid_for(M * C / 4), kThreads, 0, s>>>((const float*)dout, (const float*)out,
+                                                                          (const float*)y, mean, invstd, coef,
+                                                                          (float*)dy, (float*)dz_out, M, C);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}

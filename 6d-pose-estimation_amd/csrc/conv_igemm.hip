@@ -1,0 +1,400 @@
+// Implicit-GEMM convolution (forward and data-gradient) on MFMA for gfx950.
+//
+// Replaces the cuDNN convolutions behind torchvision's ResNet50 trunk (used by
+// every reference model, e.g. pose_net_rgbd_geometric.py:23-25) and the z-CNN of
+// pose_net_rgb_geometric.py:36-55.
+//
+// GEMM view (NHWC activations, K ordered (kh, kw, c) with c fastest):
+//   forward : Y[m = (n,oy,ox)][co] = sum_k A[m][k] * Wp[co][k],  A = im2col(X)
+//   dgrad   : dX[m = (n,y,x)][ci]  = sum_k A[m][k] * Wt[ci][k],  A = col2im-gather(dY)
+// One 256-thread workgroup = 4 waves (2 x 2) computes a BM x BN tile; K advances
+// 64 bytes per step (BK = 32 bf16 / 16 fp32) through a double-buffered,
+// XOR-swizzled LDS image (register staged so that padding taps load zeros).
+// MFMA: v_mfma_f32_16x16x32_bf16 (bf16) or v_mfma_f32_16x16x4_f32 (fp32, exact
+// fp32 products; used for the fp32 parity path).  Every lane reads its A and B
+// fragments with one ds_read_b128 each; the swizzle makes those conflict-free.
+// Epilogue: + bias, per-wave BatchNorm partial statistics (sum, sum of squares of
+// the fp32 accumulators -> stats workspace, reduced by pose6d_bn_finalize), the
+// tile goes through LDS so that global stores are whole 16-byte chunks of
+// contiguous NHWC rows, optionally adding a residual tensor (dgrad: dX += dRes).
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+template <typename T> struct KT;
+template <> struct KT<bf16> { static constexpr int VEC = 8; static constexpr int BK = 32; };
+template <> struct KT<float> { static constexpr int VEC = 4; static constexpr int BK = 16; };
+
+enum Mode { kGemm = 0, kFwd = 1, kFwdNarrow = 2, kDgrad = 3 };
+
+struct Geom {
+  int M, Ncols, K, Kpad;   // GEMM dims; Kpad = weight row length
+  int SH, SW, SC, log2SC;  // gathered source tensor (NHWC)
+  int RH, RW;              // row grid: m = (n * RH + y) * RW + x
+  int KH, KW, stride, pad;
+  int gm, gn;              // grid in tiles
+};
+
+// ds_read_b128 fragment reads: lanes (row = l & 15, chunk = l >> 4) of a 16-row
+// block; this XOR makes every 16-lane LDS group hit 16 distinct 16-byte slots.
+__device__ __forceinline__ int swz(int row) { return (4 - ((row >> 2) & 3)) & 3; }
+
+template <typename T, int BM, int BN, int MODE>
+__global__ __launch_bounds__(kThreads) void conv_igemm_kernel(const T* __restrict__ src, const T* __restrict__ wts,
+                                                              const float* __restrict__ bias, const T* __restrict__ res,
+                                                              T* __restrict__ out, float* __restrict__ stats, Geom g) {
+  constexpr int VEC = KT<T>::VEC;
+  constexpr int BK = KT<T>::BK;
+  constexpr int TM = BM / 32;            // 16x16 tiles per wave along M (waves 2 x 2)
+  constexpr int TN = BN / 32;
+  constexpr int A_PER = BM / 64;         // 16-B chunks per thread per A stage
+  constexpr int B_PER = BN / 64;
+  constexpr int STAGE = (BM + BN) * 64;  // bytes per LDS buffer
+  constexpr int CROW = BN * (int)sizeof(T) + 16;  // epilogue tile row stride (bytes)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  // XCD-aware remap: consecutive logical tiles (same M rows) share an XCD's L2.
+  const int nwg = g.gm * g.gn;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int tm = bid / g.gn, tn = bid - tm * g.gn;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ck = tid & 3;  // this thread's 16-B chunk within a 64-B row segment
+
+  // ---- per-thread A rows (fixed over K) ----
+  int a_pix[A_PER], a_y[A_PER], a_x[A_PER];
+  bool a_ok[A_PER];
+#pragma unroll
+  for (int i = 0; i < A_PER; ++i) {
+    const int m = m0 + (tid >> 2) + 64 * i;
+    a_ok[i] = m < g.M;
+    const int mm = a_ok[i] ? m : 0;
+    if (MODE == kGemm) {
+      a_pix[i] = mm; a_y[i] = 0; a_x[i] = 0;
+    } else {
+      const int hw = g.RH * g.RW;
+      const int n = mm / hw, rem = mm - n * hw;
+      const int y = rem / g.RW, x = rem - y * g.RW;
+      a_pix[i] = n * g.SH * g.SW;
+      if (MODE == kDgrad) { a_y[i] = y + g.pad; a_x[i] = x + g.pad; }
+      else { a_y[i] = y * g.stride - g.pad; a_x[i] = x * g.stride - g.pad; }
+    }
+  }
+  // ---- per-thread B rows ----
+  const T* b_ptr[B_PER];
+  bool b_ok[B_PER];
+#pragma unroll
+  for (int i = 0; i < B_PER; ++i) {
+    const int n = n0 + (tid >> 2) + 64 * i;
+    b_ok[i] = n < g.Ncols;
+    b_ptr[i] = wts + (int64_t)(b_ok[i] ? n : 0) * g.Kpad + ck * VEC;
+  }
+
+  const int nk = g.Kpad / BK;
+  uint4 ra[A_PER], rb[B_PER];
+
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i)
+      rb[i] = b_ok[i] ? *reinterpret_cast<const uint4*>(b_ptr[i] + k0) : make_uint4(0, 0, 0, 0);
+    if (MODE == kGemm) {
+#pragma unroll
+      for (int i = 0; i < A_PER; ++i)
+        ra[i] = a_ok[i] ? *reinterpret_cast<const uint4*>(src + (int64_t)a_pix[i] * g.K + k0 + ck * VEC)
+                        : make_uint4(0, 0, 0, 0);
+    } else if (MODE == kFwd || MODE == kDgrad) {
+      const int tap = k0 >> g.log2SC, c0 = k0 & (g.SC - 1);
+      const int kh = tap / g.KW, kw = tap - kh * g.KW;
+#pragma unroll
+      for (int i = 0; i < A_PER; ++i) {
+        int sy, sx;
+        bool ok = a_ok[i] && k0 < g.K;
+        if (MODE == kFwd) {
+          sy = a_y[i] + kh; sx = a_x[i] + kw;
+        } else {
+          const int ty = a_y[i] - kh, tx = a_x[i] - kw;
+          ok = ok && ty >= 0 && tx >= 0;
+          if (g.stride == 2) { ok = ok && !(ty & 1) && !(tx & 1); sy = ty >> 1; sx = tx >> 1; }
+          else { sy = ty; sx = tx; }
+        }
+        ok = ok && (unsigned)sy < (unsigned)g.SH && (unsigned)sx < (unsigned)g.SW;
+        ra[i] = ok ? *reinterpret_cast<const uint4*>(src + ((int64_t)(a_pix[i] + sy * g.SW + sx) << g.log2SC) + c0 +
+                                                     ck * VEC)
+                   : make_uint4(0, 0, 0, 0);
+      }
+    } else {  // kFwdNarrow: SC == 4 channels per tap (stem, Cin padded 3 -> 4)
+      constexpr int UNITS = VEC / 4;       // taps per 16-B chunk (bf16: 2, fp32: 1)
+#pragma unroll
+      for (int i = 0; i < A_PER; ++i) {
+        uint32_t w[4];
+#pragma unroll
+        for (int u = 0; u < UNITS; ++u) {
+          const int k = k0 + ck * VEC + u * 4;
+          const int tap = k >> 2;
+          const int kh = tap / g.KW, kw = tap - kh * g.KW;
+          const int sy = a_y[i] + kh, sx = a_x[i] + kw;
+          const bool ok = a_ok[i] && k < g.K && (unsigned)sy < (unsigned)g.SH && (unsigned)sx < (unsigned)g.SW;
+          const T* p = src + ((int64_t)(a_pix[i] + sy * g.SW + sx) << 2);
+          if (UNITS == 2) {
+            uint2 v = ok ? *reinterpret_cast<const uint2*>(p) : make_uint2(0, 0);
+            w[2 * u] = v.x; w[2 * u + 1] = v.y;
+          } else {
+            uint4 v = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+          }
+        }
+        ra[i] = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    char* As = smem + buf * STAGE;
+    char* Bs = As + BM * 64;
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int row = (tid >> 2) + 64 * i;
+      *reinterpret_cast<uint4*>(As + row * 64 + ((ck ^ swz(row)) << 4)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+      const int row = (tid >> 2) + 64 * i;
+      *reinterpret_cast<uint4*>(Bs + row * 64 + ((ck ^ swz(row)) << 4)) = rb[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fc = lane >> 4;
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + BM * 64;
+    uint4 af[TM], bfr[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wm * (BM / 2) + i * 16 + fr;
+      af[i] = *reinterpret_cast<const uint4*>(As + row * 64 + ((fc ^ swz(row)) << 4));
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int row = wn * (BN / 2) + j * 16 + fr;
+      bfr[j] = *reinterpret_cast<const uint4*>(Bs + row * 64 + ((fc ^ swz(row)) << 4));
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (sizeof(T) == 2) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
+                                                              __builtin_bit_cast(bf16x8, bfr[j]), acc[i][j], 0, 0, 0);
+        } else {
+          const f32x4 a4 = __builtin_bit_cast(f32x4, af[i]);
+          const f32x4 b4 = __builtin_bit_cast(f32x4, bfr[j]);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[s], b4[s], acc[i][j], 0, 0, 0);
+        }
+      }
+  };
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tile(kt + 1);
+    compute(cur);
+    if (kt + 1 < nk) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---------------- epilogue ----------------
+  const int row_base = m0 + wm * (BM / 2);
+  const int col_base = n0 + wn * (BN / 2);
+  if (bias) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int c = col_base + j * 16 + fr;
+      const float bv = c < g.Ncols ? bias[c] : 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[i][j] += bv;
+    }
+  }
+  if (stats) {
+    // per-wave partial sums over this wave's rows; workspace row = (tm * 2 + wm)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = row_base + i * 16 + fc * 4 + r;
+          const float v = m < g.M ? acc[i][j][r] : 0.f;
+          s += v;
+          q = fmaf(v, v, q);
+        }
+      s += __shfl_xor(s, 16, 64); q += __shfl_xor(q, 16, 64);
+      s += __shfl_xor(s, 32, 64); q += __shfl_xor(q, 32, 64);
+      const int c = col_base + j * 16 + fr;
+      if (lane < 16 && c < g.Ncols) {
+        float* sp = stats + (int64_t)(tm * 2 + wm) * 2 * g.Ncols;
+        sp[c] = s;
+        sp[g.Ncols + c] = q;
+      }
+    }
+  }
+  // stage the tile through LDS (staging buffers are dead after the final barrier)
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lr = wm * (BM / 2) + i * 16 + fc * 4 + r;
+        const int lc = wn * (BN / 2) + j * 16 + fr;
+        *reinterpret_cast<T*>(smem + lr * CROW + lc * (int)sizeof(T)) = p6::from_f<T>(acc[i][j][r]);
+      }
+  __syncthreads();
+  constexpr int CPR = BN * (int)sizeof(T) / 16;  // 16-B chunks per tile row
+  for (int idx = tid; idx < BM * CPR; idx += kThreads) {
+    const int lr = idx / CPR, cc = idx - lr * CPR;
+    const int m = m0 + lr, c = n0 + cc * (16 / (int)sizeof(T));
+    if (m >= g.M || c >= g.Ncols) continue;
+    uint4 v = *reinterpret_cast<const uint4*>(smem + lr * CROW + cc * 16);
+    T* dst = out + (int64_t)m * g.Ncols + c;
+    if (res) {
+      const uint4 rv = *reinterpret_cast<const uint4*>(res + (int64_t)m * g.Ncols + c);
+      constexpr int E = 16 / (int)sizeof(T);
+      T a[E], b[E];
+      __builtin_memcpy(a, &v, 16);
+      __builtin_memcpy(b, &rv, 16);
+#pragma unroll
+      for (int e = 0; e < E; ++e) a[e] = p6::from_f<T>(p6::to_f(a[e]) + p6::to_f(b[e]));
+      __builtin_memcpy(&v, a, 16);
+    }
+    *reinterpret_cast<uint4*>(dst) = v;
+  }
+}
+
+template <typename T, int BM, int BN, int MODE>
+int launch_t(const Geom& g0, const void* src, const void* w, const float* bias, const void* res, void* out,
+             float* stats, hipStream_t s) {
+  Geom g = g0;
+  g.gm = p6::ceil_div(g.M, BM);
+  g.gn = p6::ceil_div(g.Ncols, BN);
+  const int stage = 2 * (BM + BN) * 64;
+  const int epi = BM * (BN * (int)sizeof(T) + 16);
+  const int lds = stage > epi ? stage : epi;
+  conv_igemm_kernel<T, BM, BN, MODE><<<g.gm * g.gn, kThreads, lds, s>>>(
+      (const T*)src, (const T*)w, bias, (const T*)res, (T*)out, stats, g);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+template <typename T, int MODE>
+int launch_mode(const Geom& g, int tile, const void* src, const void* w, const float* bias, const void* res,
+                void* out, float* stats, hipStream_t s) {
+  switch (tile) {
+    case 0: return launch_t<T, 128, 128, MODE>(g, src, w, bias, res, out, stats, s);
+    case 1: return launch_t<T, 128, 64, MODE>(g, src, w, bias, res, out, stats, s);
+    case 2: return launch_t<T, 64, 128, MODE>(g, src, w, bias, res, out, stats, s);
+    default: return launch_t<T, 64, 64, MODE>(g, src, w, bias, res, out, stats, s);
+  }
+}
+
+// tile choice: the biggest tile that still gives >= 2 waves of workgroups per CU-pass
+int pick_tile(int M, int N) {
+  auto blocks = [&](int bm, int bn) { return (int64_t)p6::ceil_div(M, bm) * p6::ceil_div(N, bn); };
+  if (N <= 64) return blocks(128, 64) >= 512 ? 1 : 3;
+  if (blocks(128, 128) >= 512) return 0;
+  if (blocks(128, 64) >= 512) return 1;
+  if (blocks(64, 128) >= 512) return 2;
+  return 3;
+}
+
+int ilog2(int v) {
+  int r = 0;
+  while ((1 << r) < v) ++r;
+  return (1 << r) == v ? r : -1;
+}
+
+template <typename T>
+int dispatch(int mode, const Geom& g, int tile, const void* src, const void* w, const float* bias, const void* res,
+             void* out, float* stats, hipStream_t s) {
+  switch (mode) {
+    case kGemm: return launch_mode<T, kGemm>(g, tile, src, w, bias, res, out, stats, s);
+    case kFwd: return launch_mode<T, kFwd>(g, tile, src, w, bias, res, out, stats, s);
+    case kFwdNarrow: return launch_mode<T, kFwdNarrow>(g, tile, src, w, bias, res, out, stats, s);
+    default: return launch_mode<T, kDgrad>(g, tile, src, w, bias, res, out, stats, s);
+  }
+}
+
+}  // namespace
+
+extern "C" int pose6d_conv_stats_rows(int32_t N, int32_t Ho, int32_t Wo, int32_t Cout) {
+  const int M = N * Ho * Wo;
+  const int tile = pick_tile(M, Cout);
+  const int bm = (tile == 0 || tile == 1) ? 128 : 64;
+  return 2 * p6::ceil_div(M, bm);
+}
+
+extern "C" int pose6d_conv2d_fwd(int32_t dtype, const void* x, const void* w, const float* bias, void* y,
+                                 float* stats, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH,
+                                 int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, void* stream) {
+  P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_fwd: bad dtype %d", dtype);
+  P6_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cout > 0 && Cout % 8 == 0, "pose6d_conv2d_fwd: bad shape (Cout %% 8)");
+  P6_CHECK_ARG(Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1,
+               "pose6d_conv2d_fwd: Ho/Wo inconsistent");
+  const int bk = dtype == POSE6D_DT_BF16 ? 32 : 16;
+  const int lc = ilog2(Cin);
+  Geom g{};
+  g.M = N * Ho * Wo; g.Ncols = Cout; g.K = KH * KW * Cin;
+  g.Kpad = p6::ceil_div(g.K, bk) * bk;
+  g.SH = H; g.SW = W; g.SC = Cin; g.log2SC = lc; g.RH = Ho; g.RW = Wo;
+  g.KH = KH; g.KW = KW; g.stride = stride; g.pad = pad;
+  int mode;
+  if (KH == 1 && KW == 1 && stride == 1 && pad == 0) mode = kGemm;
+  else if (Cin == 4) mode = kFwdNarrow;
+  else {
+    P6_CHECK_ARG(lc >= 0 && Cin % bk == 0, "pose6d_conv2d_fwd: Cin must be 4 or a power of two >= %d (got %d)", bk, Cin);
+    mode = kFwd;
+  }
+  if (mode == kGemm) P6_CHECK_ARG(Cin % bk == 0, "pose6d_conv2d_fwd: 1x1 Cin %% %d != 0", bk);
+  const int tile = pick_tile(g.M, Cout);
+  hipStream_t s = p6::stream_of(stream);
+  return dtype == POSE6D_DT_BF16 ? dispatch<bf16>(mode, g, tile, x, w, bias, nullptr, y, stats, s)
+                                 : dispatch<float>(mode, g, tile, x, w, bias, nullptr, y, stats, s);
+}
+
+extern "C" int pose6d_conv2d_dgrad(int32_t dtype, const void* dy, const void* wt, const void* dres, void* dx,
+                                   int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW,
+                                   int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, void* stream) {
+  P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_dgrad: bad dtype %d", dtype);
+  P6_CHECK_ARG(stride == 1 || stride == 2, "pose6d_conv2d_dgrad: stride must be 1 or 2");
+  P6_CHECK_ARG(Cin % 8 == 0, "pose6d_conv2d_dgrad: Cin %% 8 != 0 (no data gradient for the stem)");
+  const int bk = dtype == POSE6D_DT_BF16 ? 32 : 16;
+  const int lc = ilog2(Cout);
+  P6_CHECK_ARG(lc >= 0 && Cout % bk == 0, "pose6d_conv2d_dgrad: Cout must be a power of two >= %d", bk);
+  Geom g{};
+  g.M = N * H * W; g.Ncols = Cin; g.K = KH * KW * Cout; g.Kpad = g.K;
+  g.SH = Ho; g.SW = Wo; g.SC = Cout; g.log2SC = lc; g.RH = H; g.RW = W;
+  g.KH = KH; g.KW = KW; g.stride = stride; g.pad = pad;
+  const int mode = (KH == 1 && KW == 1 && stride == 1 && pad == 0) ? kGemm : kDgrad;
+  const int tile = pick_tile(g.M, Cin);
+  hipStream_t s = p6::stream_of(stream);
+  return dtype == POSE6D_DT_BF16 ? dispatch<bf16>(mode, g, tile, dy, wt, nullptr, dres, dx, nullptr, s)
+                                 : dispatch<float>(mode, g, tile, dy, wt, nullptr, dres, dx, nullptr, s);
+}

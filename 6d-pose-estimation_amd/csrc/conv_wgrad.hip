@@ -1,0 +1,321 @@
+// Convolution weight gradient on MFMA (split-K over output pixels) for gfx950.
+//
+//   dW[co][k] = sum_m dY[m][co] * im2col(X)[m][k],   k = (kh, kw, ci), m = (n, oy, ox)
+//
+// Both operands are m-major in HBM (NHWC), so each LDS stage holds a [32 m][cols]
+// image of dY and of the gathered X, written as 16-byte rows; the MFMA operands
+// need 8 consecutive m per lane and come out of LDS through the gfx950 hardware
+// transpose read (ds_read_b64_tr_b16: 4 m x 1 column per lane per read).  The
+// XOR swizzle puts the 8 rows one 32-lane half reads on 8 distinct bank octets.
+// The reduction over m (up to 100k pixels) is split over workgroups; each split
+// writes an fp32 slab [S][Cout][Kpad] and pose6d_conv2d_wgrad_reduce sums the
+// slabs in fixed order into the OIHW fp32 gradient (deterministic, no atomics).
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int MT = 32;  // m rows per reduction step
+
+template <typename T> struct WT;
+template <> struct WT<bf16> { static constexpr int VEC = 8; };
+template <> struct WT<float> { static constexpr int VEC = 4; };
+
+struct WGeom {
+  int M, Cout, K, Kpad;
+  int SH, SW, SC, log2SC;
+  int RH, RW;
+  int KH, KW, stride, pad;
+  int gm, gn, splits, mps;  // tiles over Cout, over K; splits; m per split (multiple of MT)
+};
+
+// XOR (in 16-B chunk units, always even: keeps 32-B pairs together) for a row of
+// `pairs` 32-byte pairs, such that rows {0..3, 8..11} (and {4..7, 12..15}) of a
+// transposed read land on distinct bank octets.
+template <int PAIRS>
+__device__ __forceinline__ int swz_tr(int m) {
+  if constexpr (PAIRS >= 8) return ((m & 3) | (((m >> 3) & 1) << 2)) << 1;
+  else if constexpr (PAIRS == 4) return (((m >> 1) & 1) | (((m >> 3) & 1) << 1)) << 1;
+  else return 0;
+}
+
+// 8 consecutive m (8*grp .. 8*grp+7) of one LDS column, as an MFMA bf16 operand:
+// two ds_read_b64_tr_b16, lane 4q+p of each 16-lane group addressing row q, cols 4p..4p+3.
+template <int ROWB>
+__device__ __forceinline__ bf16x8 tr_frag(const char* img, int col, int grp, int q) {
+  bf16x8 f;
+  const int cchunk = col >> 3, cin = (col & 7) * 2;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = 8 * grp + 4 * h + q;
+    const char* a = img + r * ROWB + ((cchunk ^ swz_tr<ROWB / 32>(r)) << 4) + cin;
+    const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)a);
+    const bf16x4 bv = __builtin_bit_cast(bf16x4, v);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) f[4 * h + e] = bv[e];
+  }
+  return f;
+}
+
+template <typename T, int BM, int BN>
+__global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                              float* __restrict__ ws, WGeom g) {
+  constexpr int VEC = WT<T>::VEC;
+  constexpr bool BF = sizeof(T) == 2;
+  constexpr int YROW = BM * (int)sizeof(T);   // bytes per LDS row of the dY image
+  constexpr int XROW = BN * (int)sizeof(T);
+  constexpr int YCPR = YROW / 16, XCPR = XROW / 16;  // 16-B chunks per row
+  constexpr int YPER = MT * YCPR / kThreads, XPER = MT * XCPR / kThreads;
+  constexpr int YRSTEP = kThreads / YCPR, XRSTEP = kThreads / XCPR;
+  constexpr int STAGE = MT * (YROW + XROW);
+  constexpr int TM = BM / 32, TN = BN / 32;
+  static_assert(YPER >= 1 && XPER >= 1, "tile too small");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tiles = g.gm * g.gn;
+  const int split = blockIdx.x / tiles;
+  int t2 = blockIdx.x - split * tiles;
+  const int tm = t2 / g.gn, tn = t2 - tm * g.gn;
+  const int co0 = tm * BM, k0 = tn * BN;
+  const int mbeg = split * g.mps;
+  const int mend = min(g.M, mbeg + g.mps);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // dY loads: row yr + i*YRSTEP, chunk yc
+  const int yc = tid % YCPR, yr = tid / YCPR;
+  const bool y_ok = co0 + yc * VEC < g.Cout;
+  // X loads: chunk xc fixed -> its tap and channel are fixed for the whole loop
+  const int xc = tid % XCPR, xr = tid / XCPR;
+  const int kx = k0 + xc * VEC;
+  const bool x_kok = kx < g.K;
+  const int tap = x_kok ? (kx >> g.log2SC) : 0;
+  const int ci = kx & (g.SC - 1);
+  const int kh = tap / g.KW, kw = tap - kh * g.KW;
+  // incremental (n, oy, ox) of this thread's X rows
+  int xn[XPER], xy[XPER], xx[XPER];
+#pragma unroll
+  for (int i = 0; i < XPER; ++i) {
+    const int m = mbeg + xr + i * XRSTEP;
+    const int hw = g.RH * g.RW;
+    xn[i] = m / hw;
+    const int rem = m - xn[i] * hw;
+    xy[i] = rem / g.RW;
+    xx[i] = rem - xy[i] * g.RW;
+  }
+
+  uint4 ry[YPER], rx[XPER];
+  auto load = [&](int mstep) {
+#pragma unroll
+    for (int i = 0; i < YPER; ++i) {
+      const int m = mstep + yr + i * YRSTEP;
+      ry[i] = (y_ok && m < mend) ? *reinterpret_cast<const uint4*>(dy + (int64_t)m * g.Cout + co0 + yc * VEC)
+                                 : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < XPER; ++i) {
+      const int m = mstep + xr + i * XRSTEP;
+      const int sy = xy[i] * g.stride - g.pad + kh, sx = xx[i] * g.stride - g.pad + kw;
+      const bool ok = x_kok && m < mend && (unsigned)sy < (unsigned)g.SH && (unsigned)sx < (unsigned)g.SW;
+      const int64_t off = (((int64_t)xn[i] * g.SH + sy) * g.SW + sx) * g.SC + ci;
+      if (VEC * (int)sizeof(T) == 16 && g.SC >= VEC) {
+        rx[i] = ok ? *reinterpret_cast<const uint4*>(x + off) : make_uint4(0, 0, 0, 0);
+      } else {  // stem (SC == 4, bf16): two 4-channel taps per chunk
+        uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int k = kx + 4 * u, tp = k >> 2;
+          const int h2 = tp / g.KW, w2 = tp - h2 * g.KW;
+          const int sy2 = xy[i] * g.stride - g.pad + h2, sx2 = xx[i] * g.stride - g.pad + w2;
+          if (m < mend && k < g.K && (unsigned)sy2 < (unsigned)g.SH && (unsigned)sx2 < (unsigned)g.SW) {
+            const uint2 v = *reinterpret_cast<const uint2*>(x + (((int64_t)xn[i] * g.SH + sy2) * g.SW + sx2) * 4);
+            w[2 * u] = v.x; w[2 * u + 1] = v.y;
+          }
+        }
+        rx[i] = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      // advance this row by MT pixels
+      xx[i] += MT;
+      while (xx[i] >= g.RW) { xx[i] -= g.RW; if (++xy[i] == g.RH) { xy[i] = 0; ++xn[i]; } }
+    }
+  };
+  auto store = [&](int buf) {
+    char* Ys = smem + buf * STAGE;
+    char* Xs = Ys + MT * YROW;
+#pragma unroll
+    for (int i = 0; i < YPER; ++i) {
+      const int r = yr + i * YRSTEP;
+      const int pc = BF ? (yc ^ swz_tr<YROW / 32>(r)) : yc;
+      *reinterpret_cast<uint4*>(Ys + r * YROW + pc * 16) = ry[i];
+    }
+#pragma unroll
+    for (int i = 0; i < XPER; ++i) {
+      const int r = xr + i * XRSTEP;
+      const int pc = BF ? (xc ^ swz_tr<XROW / 32>(r)) : xc;
+      *reinterpret_cast<uint4*>(Xs + r * XROW + pc * 16) = rx[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  auto compute = [&](int buf) {
+    const char* Ys = smem + buf * STAGE;
+    const char* Xs = Ys + MT * YROW;
+    if constexpr (BF) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = tr_frag<YROW>(Ys, wm * (BM / 2) + i * 16 + 4 * p, grp, q);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = tr_frag<XROW>(Xs, wn * (BN / 2) + j * 16 + 4 * p, grp, q);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int s = 0; s < MT / 4; ++s) {
+        const int r = 4 * s + grp;
+        float a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          a[i] = *reinterpret_cast<const float*>(Ys + r * YROW + (wm * (BM / 2) + i * 16 + li) * 4);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          b[j] = *reinterpret_cast<const float*>(Xs + r * XROW + (wn * (BN / 2) + j * 16 + li) * 4);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  const int nsteps = (mend - mbeg + MT - 1) / MT;
+  if (nsteps > 0) {
+    load(mbeg);
+    store(0);
+    __syncthreads();
+    for (int st = 0; st < nsteps; ++st) {
+      const int cur = st & 1;
+      if (st + 1 < nsteps) load(mbeg + (st + 1) * MT);
+      compute(cur);
+      if (st + 1 < nsteps) store(cur ^ 1);
+      __syncthreads();
+    }
+  }
+  // slab write: rows co, cols k (C/D map: col = lane & 15, row = 4 * (lane >> 4) + r)
+  float* slab = ws + (int64_t)split * g.Cout * g.Kpad;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wm * (BM / 2) + i * 16 + grp * 4 + r;
+        const int k = k0 + wn * (BN / 2) + j * 16 + li;
+        if (co < g.Cout && k < g.Kpad) slab[(int64_t)co * g.Kpad + k] = acc[i][j][r];
+      }
+}
+
+// sum the split slabs (fixed order) into the OIHW fp32 gradient; k = (kh, kw, ci)
+__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw, int Cout, int Kpad, int SC,
+                                    int Cin, int KH, int KW, int splits, int accumulate) {
+  const int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int K = KH * KW * SC;
+  if (idx >= (int64_t)Cout * K) return;
+  const int co = idx / K, k = idx - (int64_t)co * K;
+  const int tap = k / SC, ci = k - tap * SC;
+  if (ci >= Cin) return;
+  float s = 0.f;
+  for (int i = 0; i < splits; ++i) s += ws[((int64_t)i * Cout + co) * Kpad + k];
+  const int kh = tap / KW, kw = tap - kh * KW;
+  float* d = dw + (((int64_t)co * Cin + ci) * KH + kh) * KW + kw;
+  *d = accumulate ? *d + s : s;
+}
+
+struct Plan {
+  int bm, bn, splits, mps;
+};
+
+Plan plan(int M, int Cout, int Kpad) {
+  Plan p;
+  p.bm = Cout >= 128 ? 128 : 64;
+  p.bn = Kpad >= 128 ? 128 : 64;
+  const int tiles = p6::ceil_div(Cout, p.bm) * p6::ceil_div(Kpad, p.bn);
+  // aim for ~1024 workgroups, each reducing >= 256 pixels
+  int splits = p6::ceil_div(1024, tiles);
+  const int max_splits = p6::ceil_div(M, 256);
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  int mps = p6::ceil_div(p6::ceil_div(M, splits), MT) * MT;
+  splits = p6::ceil_div(M, mps);
+  p.splits = splits;
+  p.mps = mps;
+  return p;
+}
+
+template <typename T, int BM, int BN>
+int launch(const WGeom& g, const void* x, const void* dy, float* ws, hipStream_t s) {
+  const int lds = 2 * MT * (BM + BN) * (int)sizeof(T);
+  conv_wgrad_kernel<T, BM, BN><<<g.gm * g.gn * g.splits, kThreads, lds, s>>>((const T*)x, (const T*)dy, ws, g);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+template <typename T>
+int launch_any(const WGeom& g, int bm, int bn, const void* x, const void* dy, float* ws, hipStream_t s) {
+  if (bm == 128 && bn == 128) return launch<T, 128, 128>(g, x, dy, ws, s);
+  if (bm == 128) return launch<T, 128, 64>(g, x, dy, ws, s);
+  if (bn == 128) return launch<T, 64, 128>(g, x, dy, ws, s);
+  return launch<T, 64, 64>(g, x, dy, ws, s);
+}
+
+int ilog2(int v) {
+  int r = 0;
+  while ((1 << r) < v) ++r;
+  return (1 << r) == v ? r : -1;
+}
+
+}  // namespace
+
+extern "C" int64_t pose6d_conv2d_wgrad_workspace(int32_t dtype, int32_t N, int32_t Ho, int32_t Wo, int32_t Cin,
+                                                 int32_t Cout, int32_t KH, int32_t KW) {
+  const int bk = dtype == POSE6D_DT_BF16 ? 32 : 16;
+  const int K = KH * KW * Cin;
+  const int Kpad = p6::ceil_div(K, bk) * bk;
+  const Plan p = plan(N * Ho * Wo, Cout, Kpad);
+  return (int64_t)p.splits * Cout * Kpad * 4;
+}
+
+extern "C" int pose6d_conv2d_wgrad(int32_t dtype, const void* x, const void* dy, float* dw, int32_t accumulate,
+                                   float* workspace, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cin_real,
+                                   int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho,
+                                   int32_t Wo, void* stream) {
+  P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_wgrad: bad dtype %d", dtype);
+  const int lc = ilog2(Cin);
+  P6_CHECK_ARG(lc >= 2 && Cout % 8 == 0 && Cin_real <= Cin, "pose6d_conv2d_wgrad: Cin must be a power of two >= 4");
+  const int bk = dtype == POSE6D_DT_BF16 ? 32 : 16;
+  P6_CHECK_ARG(dtype == POSE6D_DT_BF16 || Cin % 4 == 0, "pose6d_conv2d_wgrad: bad Cin");
+  WGeom g{};
+  g.M = N * Ho * Wo; g.Cout = Cout; g.K = KH * KW * Cin; g.Kpad = p6::ceil_div(g.K, bk) * bk;
+  g.SH = H; g.SW = W; g.SC = Cin; g.log2SC = lc; g.RH = Ho; g.RW = Wo;
+  g.KH = KH; g.KW = KW; g.stride = stride; g.pad = pad;
+  const Plan p = plan(g.M, Cout, g.Kpad);
+  g.gm = p6::ceil_div(Cout, p.bm); g.gn = p6::ceil_div(g.Kpad, p.bn);
+  g.splits = p.splits; g.mps = p.mps;
+  hipStream_t s = p6::stream_of(stream);
+  int rc = dtype == POSE6D_DT_BF16 ? launch_any<bf16>(g, p.bm, p.bn, x, dy, workspace, s)
+                                   : launch_any<float>(g, p.bm, p.bn, x, dy, workspace, s);
+  if (rc) return rc;
+  const int64_t total = (int64_t)Cout * g.K;
+  wgrad_reduce_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(workspace, dw, Cout, g.Kpad, Cin, Cin_real, KH,
+                                                                      KW, g.splits, accumulate);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}

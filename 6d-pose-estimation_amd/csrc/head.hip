@@ -1,0 +1,251 @@
+// Fully-connected pose heads (fp32): Linear fwd/bwd as one strided GEMM kernel,
+// BatchNorm1d (+ReLU +Dropout) fused per column, bias gradients.
+// Replaces the nn.Linear / nn.BatchNorm1d / nn.ReLU / nn.Dropout stacks of
+// pose_net_rgb.py:23-50, pose_net_rgb_geometric.py:23-33,58-65,
+// pose_net_rgbd_geometric.py:28-38.  M (batch) is 32 per GPU, so these are skinny
+// GEMMs bound by reading the weight matrix once (8 MB for 2048x1024 fp32).
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int TBM = 32, TBN = 64, TBK = 32;
+
+// C[m][n] = alpha * sum_k A(m,k) B(k,n) + (bias ? bias[n] : 0) + beta * C[m][n]
+// A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn]
+__global__ __launch_bounds__(kThreads) void gemm_f32_kernel(const float* __restrict__ A, int64_t sam, int64_t sak,
+                                                            const float* __restrict__ B, int64_t sbk, int64_t sbn,
+                                                            float* __restrict__ C, int64_t ldc,
+                                                            const float* __restrict__ bias, int M, int N, int K,
+                                                            float alpha, float beta) {
+  __shared__ float As[TBK][TBM + 1];
+  __shared__ float Bs[TBK][TBN + 1];
+  const int m0 = blockIdx.y * TBM, n0 = blockIdx.x * TBN;
+  const int tid = threadIdx.x;
+  const int tn = tid % 16, tm = tid / 16;  // each thread: rows tm*2..+1, cols tn*4..+3
+  float acc[2][4] = {};
+  for (int k0 = 0; k0 < K; k0 += TBK) {
+    for (int i = tid; i < TBK * TBM; i += kThreads) {
+      // k fastest when A is k-contiguous, m fastest otherwise (coalescing)
+      int kk, mm;
+      if (sak == 1) { kk = i % TBK; mm = i / TBK; } else { mm = i % TBM; kk = i / TBM; }
+      const int m = m0 + mm, k = k0 + kk;
+      As[kk][mm] = (m < M && k < K) ? A[m * sam + k * sak] : 0.f;
+    }
+    for (int i = tid; i < TBK * TBN; i += kThreads) {
+      int kk, nn;
+      if (sbk == 1) { kk = i % TBK; nn = i / TBK; } else { nn = i % TBN; kk = i / TBN; }
+      const int n = n0 + nn, k = k0 + kk;
+      Bs[kk][nn] = (n < N && k < K) ? B[k * sbk + n * sbn] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int kk = 0; kk < TBK; ++kk) {
+      const float a0 = As[kk][tm * 2], a1 = As[kk][tm * 2 + 1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float b = Bs[kk][tn * 4 + j];
+        acc[0][j] = fmaf(a0, b, acc[0][j]);
+        acc[1][j] = fmaf(a1, b, acc[1][j]);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + tm * 2 + i, n = n0 + tn * 4 + j;
+      if (m < M && n < N) {
+        float v = alpha * acc[i][j];
+        if (bias) v += bias[n];
+        if (beta != 0.f) v += beta * C[m * ldc + n];
+        C[m * ldc + n] = v;
+      }
+    }
+}
+
+// db[n] (+)= sum_m dy[m][n]
+__global__ void colsum_kernel(const float* __restrict__ dy, float* __restrict__ db, int M, int N, int accumulate) {
+  const int n = blockIdx.x * kThreads + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int m = 0; m < M; ++m) s += dy[(int64_t)m * N + n];
+  db[n] = accumulate ? db[n] + s : s;
+}
+
+// counter-based uniform in [0,1): hash of (seed, index)
+__device__ __forceinline__ float uniform(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+// BatchNorm1d over the batch (one thread per column) + optional ReLU + Dropout.
+__global__ void bn1d_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int M, int C,
+                                const float* __restrict__ gamma, const float* __restrict__ beta,
+                                float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
+                                float momentum, float eps, int training, int relu, float p_drop, uint64_t seed,
+                                uint8_t* __restrict__ mask, float* __restrict__ smean, float* __restrict__ sinv) {
+  const int c = blockIdx.x * kThreads + threadIdx.x;
+  if (c >= C) return;
+  float mean, inv;
+  if (training) {
+    double s = 0.0, q = 0.0;
+    for (int m = 0; m < M; ++m) s += x[(int64_t)m * C + c];
+    mean = (float)(s / M);
+    for (int m = 0; m < M; ++m) { const double d = x[(int64_t)m * C + c] - mean; q += d * d; }
+    const double var = q / M;
+    inv = (float)(1.0 / sqrt(var + eps));
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(M > 1 ? var * M / (M - 1) : var);
+    if (c == 0 && nbt) nbt[0] += 1;
+  } else {
+    mean = rmean[c];
+    inv = 1.0f / sqrtf(rvar[c] + eps);
+  }
+  smean[c] = mean;
+  sinv[c] = inv;
+  const float g = gamma[c], b = beta[c];
+  const float keep_scale = p_drop > 0.f ? 1.0f / (1.0f - p_drop) : 1.0f;
+  for (int m = 0; m < M; ++m) {
+    const int64_t o = (int64_t)m * C + c;
+    float v = (x[o] - mean) * inv * g + b;
+    if (relu) v = fmaxf(v, 0.f);
+    if (p_drop > 0.f) {
+      const bool keep = uniform(seed, (uint64_t)o) >= p_drop;
+      mask[o] = keep;
+      v = keep ? v * keep_scale : 0.f;
+    }
+    y[o] = v;
+  }
+}
+
+// backward of bn1d_fwd (train mode: batch statistics)
+__global__ void bn1d_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                const float* __restrict__ y, int M, int C, const float* __restrict__ gamma,
+                                const float* __restrict__ smean, const float* __restrict__ sinv, int training,
+                                int relu, float p_drop, const uint8_t* __restrict__ mask, float* __restrict__ dx,
+                                float* __restrict__ dgamma, float* __restrict__ dbeta, int accumulate) {
+  const int c = blockIdx.x * kThreads + threadIdx.x;
+  if (c >= C) return;
+  const float mean = smean[c], inv = sinv[c], g = gamma[c];
+  const float keep_scale = p_drop > 0.f ? 1.0f / (1.0f - p_drop) : 1.0f;
+  double sd = 0.0, sdx = 0.0;
+  for (int m = 0; m < M; ++m) {
+    const int64_t o = (int64_t)m * C + c;
+    float d = dy[o];
+    if (p_drop > 0.f) d = mask[o] ? d * keep_scale : 0.f;
+    if (relu && !(y[o] > 0.f)) d = 0.f;
+    sd += d;
+    sdx += (double)d * ((x[o] - mean) * inv);
+  }
+  if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)sdx;
+  if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)sd;
+  const float c2 = (float)(sd / M), c3 = (float)(sdx / M);
+  for (int m = 0; m < M; ++m) {
+    const int64_t o = (int64_t)m * C + c;
+    float d = dy[o];
+    if (p_drop > 0.f) d = mask[o] ? d * keep_scale : 0.f;
+    if (relu && !(y[o] > 0.f)) d = 0.f;
+    const float xh = (x[o] - mean) * inv;
+    dx[o] = training ? g * inv * (d - c2 - xh * c3) : g * inv * d;
+  }
+}
+
+// elementwise act (+dropout) used by the plain Linear->ReLU->Dropout layers
+__global__ void act_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n, int act, float p_drop,
+                               uint64_t seed, uint8_t* __restrict__ mask) {
+  const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;
+  if (i >= n) return;
+  float v = x[i];
+  if (act == 1) v = fmaxf(v, 0.f);
+  else if (act == 2) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));  // exact GELU
+  if (p_drop > 0.f) {
+    const bool keep = uniform(seed, (uint64_t)i) >= p_drop;
+    mask[i] = keep;
+    v = keep ? v / (1.0f - p_drop) : 0.f;
+  }
+  y[i] = v;
+}
+
+__global__ void act_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x, float* __restrict__ dx,
+                               int64_t n, int act, float p_drop, const uint8_t* __restrict__ mask) {
+  const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;
+  if (i >= n) return;
+  float d = dy[i];
+  if (p_drop > 0.f) d = mask[i] ? d / (1.0f - p_drop) : 0.f;
+  const float v = x[i];
+  if (act == 1) d = v > 0.f ? d : 0.f;
+  else if (act == 2) {
+    const float cdf = 0.5f * (1.0f + erff(v * 0.70710678118654752f));
+    const float pdf = 0.39894228040143268f * expf(-0.5f * v * v);
+    d = d * (cdf + v * pdf);
+  }
+  dx[i] = d;
+}
+
+}  // namespace
+
+extern "C" int pose6d_gemm_f32(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
+                               float* C, int64_t ldc, const float* bias, int32_t M, int32_t N, int32_t K, float alpha,
+                               float beta, void* stream) {
+  P6_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "pose6d_gemm_f32: bad sizes");
+  if (M == 0 || N == 0) return POSE6D_OK;
+  dim3 grid(p6::ceil_div(N, TBN), p6::ceil_div(M, TBM));
+  gemm_f32_kernel<<<grid, kThreads, 0, p6::stream_of(stream)>>>(A, sam, sak, B, sbk, sbn, C, ldc, bias, M, N, K, alpha,
+                                                                beta);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+extern "C" int pose6d_colsum_f32(const float* dy, float* db, int32_t M, int32_t N, int32_t accumulate, void* stream) {
+  if (N == 0) return POSE6D_OK;
+  colsum_kernel<<<p6::ceil_div(N, kThreads), kThreads, 0, p6::stream_of(stream)>>>(dy, db, M, N, accumulate);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+extern "C" int pose6d_bn1d_fwd(const float* x, float* y, int32_t M, int32_t C, const float* gamma, const float* beta,
+                               float* running_mean, float* running_var, int64_t* num_batches, float momentum, float eps,
+                               int32_t training, int32_t relu, float p_drop, uint64_t seed, uint8_t* mask,
+                               float* save_mean, float* save_invstd, void* stream) {
+  P6_CHECK_ARG(M > 0 && C > 0, "pose6d_bn1d_fwd: bad sizes");
+  P6_CHECK_ARG(!training || M > 1, "Expected more than 1 value per channel when training (BatchNorm1d)");
+  P6_CHECK_ARG(p_drop == 0.f || mask, "pose6d_bn1d_fwd: dropout needs a mask buffer");
+  bn1d_fwd_kernel<<<p6::ceil_div(C, kThreads), kThreads, 0, p6::stream_of(stream)>>>(
+      x, y, M, C, gamma, beta, running_mean, running_var, num_batches, momentum, eps, training, relu, p_drop, seed, mask,
+      save_mean, save_invstd);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+extern "C" int pose6d_bn1d_bwd(const float* dy, const float* x, const float* y, int32_t M, int32_t C,
+                               const float* gamma, const float* save_mean, const float* save_invstd, int32_t training,
+                               int32_t relu, float p_drop, const uint8_t* mask, float* dx, float* dgamma, float* dbeta,
+                               int32_t accumulate, void* stream) {
+  bn1d_bwd_kernel<<<p6::ceil_div(C, kThreads), kThreads, 0, p6::stream_of(stream)>>>(
+      dy, x, y, M, C, gamma, save_mean, save_invstd, training, relu, p_drop, mask, dx, dgamma, dbeta, accumulate);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+extern "C" int pose6d_act_fwd(const float* x, float* y, int64_t n, int32_t act, float p_drop, uint64_t seed,
+                              uint8_t* mask, void* stream) {
+  if (n == 0) return POSE6D_OK;
+  act_fwd_kernel<<<(unsigned)((n + kThreads - 1) / kThreads), kThreads, 0, p6::stream_of(stream)>>>(x, y, n, act, p_drop,
+                                                                                                 seed, mask);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+extern "C" int pose6d_act_bwd(const float* dy, const float* x, float* dx, int64_t n, int32_t act, float p_drop,
+                              const uint8_t* mask, void* stream) {
+  if (n == 0) return POSE6D_OK;
+  act_bwd_kernel<<<(unsigned)((n + kThreads - 1) / kThreads), kThreads, 0, p6::stream_of(stream)>>>(dy, x, dx, n, act,
+                                                                                                 p_drop, mask);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}

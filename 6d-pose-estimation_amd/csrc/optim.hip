@@ -1,0 +1,97 @@
+// Gradient clipping + AdamW over one flat fp32 parameter buffer.
+// Replaces the callers' torch.nn.utils.clip_grad_norm_(params, 1.0) and
+// optim.AdamW(lr=1e-4, weight_decay=1e-4).step() (train_rgbd_geometric.py:65,111-112)
+// with two launches for all 26 M parameters:
+//   pose6d_sumsq_partial : fixed grid of NPART blocks, per-block sum of g^2 (fp32)
+//   pose6d_adamw_step    : every block re-reduces the NPART partials (4 KB, L2-hot)
+//                          in fixed order -> same norm everywhere, deterministic;
+//                          clip coefficient min(1, max_norm/(norm+1e-6)); AdamW
+//                          update in torch's operation order.
+// Hyper-parameters come from a device array (graph replays pick up lr changes):
+//   hp = {lr, beta1, beta2, eps, weight_decay, bias_correction1, bias_correction2, max_norm}
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__global__ __launch_bounds__(kThreads) void sumsq_kernel(const float* __restrict__ g, int64_t n,
+                                                         float* __restrict__ part) {
+  __shared__ float red[kThreads / 64];
+  float s = 0.f;
+  const int64_t n4 = n / 4;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kThreads) {
+    const float4 v = g4[i];
+    s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s); s = fmaf(v.z, v.z, s); s = fmaf(v.w, v.w, s);
+  }
+  for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads)
+    s = fmaf(g[i], g[i], s);
+  s = p6::wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(kThreads) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                         float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                         const float* __restrict__ part, int nparts,
+                                                         const float* __restrict__ hp, float* __restrict__ norm_out) {
+  __shared__ float s_coef;
+  __shared__ double red[kThreads / 64];
+  const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4], bc1 = hp[5], bc2 = hp[6], max_norm = hp[7];
+  if (max_norm > 0.f) {
+    double s = 0.0;
+    for (int i = threadIdx.x; i < nparts; i += kThreads) s += (double)part[i];
+    s = p6::wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float norm = (float)sqrt(red[0] + red[1] + red[2] + red[3]);
+      const float c = max_norm / (norm + 1e-6f);
+      s_coef = c < 1.f ? c : 1.f;
+      if (blockIdx.x == 0 && norm_out) norm_out[0] = norm;
+    }
+    __syncthreads();
+  } else if (threadIdx.x == 0) {
+    s_coef = 1.f;
+  }
+  __syncthreads();
+  const float coef = s_coef;
+  const float step_size = lr / bc1;
+  const float bc2s = sqrtf(bc2);
+  const float decay = 1.f - lr * wd;
+  for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
+    const float gi = g[i] * coef;
+    float pi = p[i] * decay;
+    float mi = m[i];
+    mi = mi + (1.f - b1) * (gi - mi);                 // exp_avg.lerp_(grad, 1 - beta1)
+    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;  // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
+    const float denom = sqrtf(vi) / bc2s + eps;
+    pi = pi - step_size * (mi / denom);
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
+}  // namespace
+
+extern "C" int pose6d_sumsq_partial(const float* g, int64_t n, float* partials, int32_t nparts, void* stream) {
+  P6_CHECK_ARG(nparts > 0 && nparts <= 65535, "pose6d_sumsq_partial: bad nparts");
+  sumsq_kernel<<<nparts, kThreads, 0, p6::stream_of(stream)>>>(g, n, partials);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+extern "C" int pose6d_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                                 const float* partials, int32_t nparts, const float* hp, float* norm_out,
+                                 void* stream) {
+  if (n == 0) return POSE6D_OK;
+  int64_t blocks = (n + kThreads * 4 - 1) / (kThreads * 4);
+  if (blocks > 4096) blocks = 4096;
+  adamw_kernel<<<(unsigned)blocks, kThreads, 0, p6::stream_of(stream)>>>(param, grad, exp_avg, exp_avg_sq, n, partials,
+                                                                        nparts, hp, norm_out);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}

@@ -96,6 +96,108 @@ int pose6d_pose_loss_bwd(const float *pred_rot, const float *pred_trans, const f
                          int32_t rot_mode, const float *dloss, float *grad_rot, float *grad_trans,
                          void *stream);
 
+/* ------------------------------------------------------------------------
+ * ResNet50 trunk — replaces torchvision.models.resnet50 children[:-1] as
+ * wrapped by every model (pose_net_rgb.py:18-20, pose_net_rgb_geometric.py:18-20,
+ * pose_net_rgbd.py:48-61, pose_net_rgbd_geometric.py:23-25) and the z-CNN of
+ * pose_net_rgb_geometric.py:36-55.  NHWC activations of `dtype`.
+ * ---------------------------------------------------------------------- */
+/* model input (B, C, H, W) fp32 -> NHWC with channels zero-padded to Cpad */
+int pose6d_nchw_to_nhwc(int32_t dtype, const float *x, void *y, int32_t N, int32_t C, int32_t H, int32_t W,
+                        int32_t Cpad, void *stream);
+
+/* One launch packs every conv's OIHW fp32 master weight into the kernel layouts:
+ * wp [O][Kpad] (K = (kh, kw, ci), ci padded to Ip, zeros beyond K) and, when
+ * non-null, wt [I][KH][KW][O] for the data gradient.  `descs` is a device array of
+ * n_desc records of pose6d_pack_desc_size() bytes:
+ *   { const float *w; void *wp; void *wt; int32 O, I, Ip, KH, KW, Kpad; int64 start, count; }
+ * with start = running sum of O*Kpad, total = sum of O*Kpad. */
+int pose6d_pack_desc_size(void);
+int pose6d_pack_conv_weights(int32_t dtype, const void *descs, int32_t n_desc, int64_t total, void *stream);
+
+/* nn.Conv2d forward (implicit GEMM on MFMA).  x [N][H][W][Cin] (Cin = 4 for the
+ * padded stem, else a power of two), wp packed [Cout][Kpad], y [N][Ho][Wo][Cout].
+ * bias may be NULL.  stats (NULL = none) receives per-wave BatchNorm partial sums:
+ * pose6d_conv_stats_rows(...) rows of [2][Cout] fp32 (sum, sum of squares). */
+int pose6d_conv_stats_rows(int32_t N, int32_t Ho, int32_t Wo, int32_t Cout);
+int pose6d_conv2d_fwd(int32_t dtype, const void *x, const void *wp, const float *bias, void *y, float *stats,
+                      int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW,
+                      int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, void *stream);
+/* data gradient: dx [N][H][W][Cin] = conv_transpose(dy [N][Ho][Wo][Cout], wt) (+ dres if non-NULL) */
+int pose6d_conv2d_dgrad(int32_t dtype, const void *dy, const void *wt, const void *dres, void *dx, int32_t N,
+                        int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
+                        int32_t pad, int32_t Ho, int32_t Wo, void *stream);
+/* weight gradient into OIHW fp32 dw (Cin_real channels of the Cin-padded input);
+ * workspace: pose6d_conv2d_wgrad_workspace(...) bytes of fp32 split slabs. */
+int64_t pose6d_conv2d_wgrad_workspace(int32_t dtype, int32_t N, int32_t Ho, int32_t Wo, int32_t Cin, int32_t Cout,
+                                      int32_t KH, int32_t KW);
+int pose6d_conv2d_wgrad(int32_t dtype, const void *x, const void *dy, float *dw, int32_t accumulate,
+                        float *workspace, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cin_real,
+                        int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
+                        void *stream);
+
+/* nn.BatchNorm2d: finalize the conv-epilogue statistics (training) or use the
+ * running statistics (eval) -> scale/shift (+ saved mean / invstd); running
+ * stats, num_batches_tracked updated in training (torch semantics). */
+int pose6d_bn_finalize(const float *partial, int32_t rows, int32_t C, int64_t count, const float *gamma,
+                       const float *beta, float *running_mean, float *running_var, int64_t *num_batches,
+                       float momentum, float eps, int32_t training, float *scale, float *shift, float *save_mean,
+                       float *save_invstd, void *stream);
+/* out = act(y * scale + shift [+ res | + res * res_scale + res_shift]); act = ReLU if relu */
+int pose6d_bn_act_fwd(int32_t dtype, const void *y, const float *scale, const float *shift, const void *res,
+                      const float *res_scale, const float *res_shift, int32_t relu, void *out, int64_t M, int32_t C,
+                      void *stream);
+/* backward of bn_act_fwd for one BN: dz = relu ? dout * (out > 0) : dout;
+ * dgamma/dbeta (accumulate or overwrite); dy; dz_out (if non-NULL) = dz.
+ * workspace: (pose6d_bn_bwd_workspace_rows(M) * 2 + 3) * C floats. */
+int pose6d_bn_bwd_workspace_rows(int64_t M);
+int pose6d_bn_bwd(int32_t dtype, const void *dout, const void *out, const void *y, const float *mean,
+                  const float *invstd, const float *gamma, float *dgamma, float *dbeta, int32_t accumulate, void *dy,
+                  void *dz_out, float *workspace, int64_t M, int32_t C, void *stream);
+
+/* nn.MaxPool2d(k, s, p) on NHWC; argmax = window index (uint8) of the first max */
+int pose6d_maxpool_fwd(int32_t dtype, const void *x, void *y, uint8_t *argmax, int32_t N, int32_t H, int32_t W,
+                       int32_t C, int32_t k, int32_t s, int32_t p, int32_t Ho, int32_t Wo, void *stream);
+int pose6d_maxpool_bwd(int32_t dtype, const void *dy, const uint8_t *argmax, void *dx, int32_t N, int32_t H,
+                       int32_t W, int32_t C, int32_t k, int32_t s, int32_t p, int32_t Ho, int32_t Wo, void *stream);
+/* nn.AdaptiveAvgPool2d(1) + view(B, -1): x [N][HW][C] -> y [N][C] fp32 */
+int pose6d_avgpool_fwd(int32_t dtype, const void *x, float *y, int32_t N, int32_t HW, int32_t C, void *stream);
+int pose6d_avgpool_bwd(int32_t dtype, const float *dy, void *dx, int32_t N, int32_t HW, int32_t C, void *stream);
+
+/* ------------------------------------------------------------------------
+ * Fully-connected heads (fp32) — nn.Linear / BatchNorm1d / ReLU / GELU / Dropout
+ * of the rot/trans/z heads (pose_net_rgb.py:23-50, pose_net_rgbd_geometric.py:28-38,
+ * pose_net_rgb_geometric.py:23-33,58-65, pose_net_rgbd.py:73-103).
+ * ---------------------------------------------------------------------- */
+/* C[m][n] = alpha * sum_k A[m*sam + k*sak] * B[k*sbk + n*sbn] (+ bias[n]) + beta * C[m][n] */
+int pose6d_gemm_f32(const float *A, int64_t sam, int64_t sak, const float *B, int64_t sbk, int64_t sbn, float *C,
+                    int64_t ldc, const float *bias, int32_t M, int32_t N, int32_t K, float alpha, float beta,
+                    void *stream);
+int pose6d_colsum_f32(const float *dy, float *db, int32_t M, int32_t N, int32_t accumulate, void *stream);
+/* BatchNorm1d (+ReLU) (+Dropout p_drop with a counter-based RNG keyed by seed) */
+int pose6d_bn1d_fwd(const float *x, float *y, int32_t M, int32_t C, const float *gamma, const float *beta,
+                    float *running_mean, float *running_var, int64_t *num_batches, float momentum, float eps,
+                    int32_t training, int32_t relu, float p_drop, uint64_t seed, uint8_t *mask, float *save_mean,
+                    float *save_invstd, void *stream);
+int pose6d_bn1d_bwd(const float *dy, const float *x, const float *y, int32_t M, int32_t C, const float *gamma,
+                    const float *save_mean, const float *save_invstd, int32_t training, int32_t relu, float p_drop,
+                    const uint8_t *mask, float *dx, float *dgamma, float *dbeta, int32_t accumulate, void *stream);
+/* act: 0 identity, 1 ReLU, 2 GELU (erf); optional dropout */
+int pose6d_act_fwd(const float *x, float *y, int64_t n, int32_t act, float p_drop, uint64_t seed, uint8_t *mask,
+                   void *stream);
+int pose6d_act_bwd(const float *dy, const float *x, float *dx, int64_t n, int32_t act, float p_drop,
+                   const uint8_t *mask, void *stream);
+
+/* ------------------------------------------------------------------------
+ * Optimiser — clip_grad_norm_(params, max_norm) + AdamW.step() of the callers
+ * (train_rgbd_geometric.py:65,111-112) over one flat fp32 buffer.
+ * hp (device) = {lr, beta1, beta2, eps, weight_decay, bias_correction1,
+ *                bias_correction2, max_norm (<= 0: no clipping)}
+ * ---------------------------------------------------------------------- */
+int pose6d_sumsq_partial(const float *g, int64_t n, float *partials, int32_t nparts, void *stream);
+int pose6d_adamw_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+                      const float *partials, int32_t nparts, const float *hp, float *norm_out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,6 +11,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 RTOL = 1e-4
 
 
+def _well_conditioned(pr, gr, kind):
+    if kind != "geodesic":
+        return np.ones(len(pr), bool)
+    q1 = pr / np.maximum(np.linalg.norm(pr.astype(np.float64), axis=1, keepdims=True), 1e-12)
+    q2 = gr / np.linalg.norm(gr.astype(np.float64), axis=1, keepdims=True)
+    q2 = np.where((q1 * q2).sum(1, keepdims=True) < 0, -q2, q2)
+    return np.linalg.norm(q1 - q2, axis=1) > 1e-5
+
+
 @pytest.mark.gpu
 def test_pose_loss_gpu_vs_reference(golden):
     from models.pose_loss import PoseLoss
@@ -28,8 +37,11 @@ def test_pose_loss_gpu_vs_reference(golden):
             key = f"{case}/{mode}"
             ref_g = g[key + "/grad_rot"]
             np.testing.assert_allclose(loss.item(), g[key + "/loss"], rtol=RTOL, atol=1e-6, err_msg=key)
-            np.testing.assert_allclose(a.grad.cpu().numpy(), ref_g, rtol=RTOL, atol=1e-6 * max(1.0, np.abs(ref_g).max()),
-                                       err_msg=key)
+            # rows where q1 == +-q2 up to rounding: ||q1 -+ q2|| ~ 1e-8 and the
+            # reference's own gradient direction is rounding noise -> not comparable
+            ok = _well_conditioned(g[f"{case}/pred_rot"], g[f"{case}/gt_rot"], kind)
+            np.testing.assert_allclose(a.grad.cpu().numpy()[ok], ref_g[ok], rtol=RTOL,
+                                       atol=1e-6 * max(1.0, np.abs(ref_g).max()), err_msg=key)
             np.testing.assert_allclose(b.grad.cpu().numpy(), g[key + "/grad_trans"], rtol=RTOL, atol=1e-7, err_msg=key)
 
 
