@@ -245,6 +245,24 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const T* __restr
   }
 }
 
+// out[c] (+)= sum_m x[m][c]  (conv-bias gradient); one block per channel chunk of 64
+template <typename T>
+__global__ __launch_bounds__(kThreads) void channel_sum_kernel(const T* __restrict__ x, int64_t M, int C,
+                                                               float* __restrict__ out, int accumulate) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, pr = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float s = 0.f;
+  if (c < C)
+    for (int64_t m = pr; m < M; m += 4) s += p6::to_f(x[m * C + c]);
+  red[pr][cl] = s;
+  __syncthreads();
+  if (pr == 0 && c < C) {
+    s = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    out[c] = accumulate ? out[c] + s : s;
+  }
+}
+
 inline unsigned grid_for(int64_t chunks) {
   int64_t b = (chunks + kThreads - 1) / kThreads;
   if (b > 4096) b = 4096;
@@ -318,6 +336,17 @@ extern "C" int pose6d_bn_bwd(int32_t dtype, const void* dout, const void* out, c
     bn_bwd_apply_kernel<float><<<grid_for(M * C / 4), kThreads, 0, s>>>((const float*)dout, (const float*)out,
                                                                           (const float*)y, mean, invstd, coef,
                                                                           (float*)dy, (float*)dz_out, M, C);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+extern "C" int pose6d_channel_sum(int32_t dtype, const void* x, int64_t M, int32_t C, float* out, int32_t accumulate,
+                                  void* stream) {
+  hipStream_t s = p6::stream_of(stream);
+  if (dtype == POSE6D_DT_BF16)
+    channel_sum_kernel<bf16><<<p6::ceil_div(C, 64), kThreads, 0, s>>>((const bf16*)x, M, C, out, accumulate);
+  else
+    channel_sum_kernel<float><<<p6::ceil_div(C, 64), kThreads, 0, s>>>((const float*)x, M, C, out, accumulate);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }

@@ -87,7 +87,7 @@ __device__ __forceinline__ float uniform(uint64_t seed, uint64_t i) {
 __global__ void bn1d_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int M, int C,
                                 const float* __restrict__ gamma, const float* __restrict__ beta,
                                 float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
-                                float momentum, float eps, int training, int relu, float p_drop, uint64_t seed,
+                                float momentum, float eps, int training, int relu, float p_drop, const uint64_t* __restrict__ seedp, uint64_t salt,
                                 uint8_t* __restrict__ mask, float* __restrict__ smean, float* __restrict__ sinv) {
   const int c = blockIdx.x * kThreads + threadIdx.x;
   if (c >= C) return;
@@ -115,7 +115,7 @@ __global__ void bn1d_fwd_kernel(const float* __restrict__ x, float* __restrict__
     float v = (x[o] - mean) * inv * g + b;
     if (relu) v = fmaxf(v, 0.f);
     if (p_drop > 0.f) {
-      const bool keep = uniform(seed, (uint64_t)o) >= p_drop;
+      const bool keep = uniform(seedp[0] ^ salt, (uint64_t)o) >= p_drop;
       mask[o] = keep;
       v = keep ? v * keep_scale : 0.f;
     }
@@ -157,14 +157,14 @@ __global__ void bn1d_bwd_kernel(const float* __restrict__ dy, const float* __res
 
 // elementwise act (+dropout) used by the plain Linear->ReLU->Dropout layers
 __global__ void act_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n, int act, float p_drop,
-                               uint64_t seed, uint8_t* __restrict__ mask) {
+                               const uint64_t* __restrict__ seedp, uint64_t salt, uint8_t* __restrict__ mask) {
   const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;
   if (i >= n) return;
   float v = x[i];
   if (act == 1) v = fmaxf(v, 0.f);
   else if (act == 2) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));  // exact GELU
   if (p_drop > 0.f) {
-    const bool keep = uniform(seed, (uint64_t)i) >= p_drop;
+    const bool keep = uniform(seedp[0] ^ salt, (uint64_t)i) >= p_drop;
     mask[i] = keep;
     v = keep ? v / (1.0f - p_drop) : 0.f;
   }
@@ -210,14 +210,14 @@ extern "C" int pose6d_colsum_f32(const float* dy, float* db, int32_t M, int32_t 
 
 extern "C" int pose6d_bn1d_fwd(const float* x, float* y, int32_t M, int32_t C, const float* gamma, const float* beta,
                                float* running_mean, float* running_var, int64_t* num_batches, float momentum, float eps,
-                               int32_t training, int32_t relu, float p_drop, uint64_t seed, uint8_t* mask,
-                               float* save_mean, float* save_invstd, void* stream) {
+                               int32_t training, int32_t relu, float p_drop, const uint64_t* seed, uint64_t salt,
+                               uint8_t* mask, float* save_mean, float* save_invstd, void* stream) {
   P6_CHECK_ARG(M > 0 && C > 0, "pose6d_bn1d_fwd: bad sizes");
   P6_CHECK_ARG(!training || M > 1, "Expected more than 1 value per channel when training (BatchNorm1d)");
-  P6_CHECK_ARG(p_drop == 0.f || mask, "pose6d_bn1d_fwd: dropout needs a mask buffer");
+  P6_CHECK_ARG(p_drop == 0.f || (mask && seed), "pose6d_bn1d_fwd: dropout needs a mask buffer and a seed");
   bn1d_fwd_kernel<<<p6::ceil_div(C, kThreads), kThreads, 0, p6::stream_of(stream)>>>(
-      x, y, M, C, gamma, beta, running_mean, running_var, num_batches, momentum, eps, training, relu, p_drop, seed, mask,
-      save_mean, save_invstd);
+      x, y, M, C, gamma, beta, running_mean, running_var, num_batches, momentum, eps, training, relu, p_drop, seed, salt,
+      mask, save_mean, save_invstd);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
@@ -232,11 +232,12 @@ extern "C" int pose6d_bn1d_bwd(const float* dy, const float* x, const float* y, 
   return POSE6D_OK;
 }
 
-extern "C" int pose6d_act_fwd(const float* x, float* y, int64_t n, int32_t act, float p_drop, uint64_t seed,
-                              uint8_t* mask, void* stream) {
+extern "C" int pose6d_act_fwd(const float* x, float* y, int64_t n, int32_t act, float p_drop, const uint64_t* seed,
+                              uint64_t salt, uint8_t* mask, void* stream) {
   if (n == 0) return POSE6D_OK;
+  P6_CHECK_ARG(p_drop == 0.f || (mask && seed), "pose6d_act_fwd: dropout needs a mask buffer and a seed");
   act_fwd_kernel<<<(unsigned)((n + kThreads - 1) / kThreads), kThreads, 0, p6::stream_of(stream)>>>(x, y, n, act, p_drop,
-                                                                                                 seed, mask);
+                                                                                                 seed, salt, mask);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }

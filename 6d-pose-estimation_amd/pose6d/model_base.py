@@ -1,0 +1,62 @@
+"""Shared plumbing of the drop-in PoseNet modules: engine bookkeeping, compute
+dtype, and the device-side dropout seed."""
+import os
+
+import torch
+import torch.nn as nn
+
+from . import autograd
+from .head import HeadEngine
+from .trunk import TrunkEngine
+
+_DTYPE_ENV = {"fp32": torch.float32, "f32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
+              "bfloat16": torch.bfloat16}
+
+
+def default_compute_dtype():
+    return _DTYPE_ENV[os.environ.get("POSE6D_COMPUTE_DTYPE", "fp32").lower()]
+
+
+class EngineModel(nn.Module):
+    """nn.Module whose children hold the reference's parameters while the math
+    runs in pose6d engines (not submodules: state_dict keys stay the reference's)."""
+
+    def _p6_init(self):
+        self._p6_dtype = default_compute_dtype()
+        self._p6_engines = {}
+        self.register_buffer("_p6_seed", torch.tensor([torch.initial_seed() & 0x7FFFFFFFFFFF], dtype=torch.int64),
+                             persistent=False)
+
+    def set_compute_dtype(self, dtype):
+        """torch.float32 (reference numerics) or torch.bfloat16 (trunk activations
+        and MFMA operands in bf16, fp32 accumulation / BN statistics / heads)."""
+        self._p6_dtype = dtype
+        return self
+
+    @property
+    def compute_dtype(self):
+        return self._p6_dtype
+
+    def _engine(self, name, factory):
+        eng = self._p6_engines.get(name)
+        if eng is None:
+            eng = factory()
+            self._p6_engines[name] = eng
+        return eng
+
+    def _run_trunk(self, name, seq, x, in_channels, kind="resnet50"):
+        eng = self._engine(name, lambda: TrunkEngine(seq, in_channels, kind))
+        eng.set_dtype(self._p6_dtype)
+        return autograd.run(eng, x, self.training, list(seq.parameters()))
+
+    def _run_head(self, name, seq, x, salt):
+        eng = self._engine(name, lambda: HeadEngine(seq))
+        return autograd.run(eng, x, self.training, list(seq.parameters()), seed_dev=self._p6_seed, salt=salt)
+
+    def _advance_seed(self):
+        if self.training:
+            with torch.no_grad():
+                self._p6_seed.add_(1)
+
+    def engines(self):
+        return dict(self._p6_engines)

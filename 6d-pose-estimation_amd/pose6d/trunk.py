@@ -1,0 +1,365 @@
+"""Convolutional trunk engine: runs a ResNet50 trunk (or the RGB-Geometric z-CNN)
+forward and backward on the pose6d HIP kernels.
+
+Replaces what torchvision/cuDNN do behind `self.backbone(x)` in every reference
+model (e.g. pose_net_rgbd_geometric.py:43) and the autograd backward of it.
+
+Design (MI355X-first):
+  * activations NHWC in `dtype` (bf16 for training throughput, fp32 for parity);
+  * every conv = one implicit-GEMM MFMA launch whose epilogue also emits the
+    BatchNorm batch-statistics partials; BN+ReLU(+residual) = one vectorised pass;
+  * conv weights: fp32 OIHW masters (the nn.Parameters, so state_dicts interchange
+    with the reference) packed to the kernel layouts by ONE launch per step;
+  * all buffers preallocated per (batch, H, W, dtype) -> the whole step is
+    graph-capturable (no allocation, no host sync inside forward/backward).
+Only one forward's activations are kept: backward() must follow the forward it
+differentiates (checked with a generation counter).
+"""
+import ctypes
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from ._lib import DT_BF16, DT_F32, Pose6dError, call, query, require_device, stream
+
+DTYPES = {torch.float32: DT_F32, torch.bfloat16: DT_BF16}
+
+
+_DESC = np.dtype([("w", "<u8"), ("wp", "<u8"), ("wt", "<u8"), ("O", "<i4"), ("I", "<i4"), ("Ip", "<i4"),
+                  ("KH", "<i4"), ("KW", "<i4"), ("Kpad", "<i4"), ("start", "<i8"), ("count", "<i8")])
+
+
+def pack_single(w, cin_pad, dtype, with_t=True):
+    """Pack one OIHW fp32 device weight -> (wp [O][Kpad], wt [Ipad][KH][KW][O] or None)."""
+    O, I, KH, KW = w.shape
+    bk = 32 if dtype == torch.bfloat16 else 16
+    Kpad = (KH * KW * cin_pad + bk - 1) // bk * bk
+    wp = torch.empty(O, Kpad, device=w.device, dtype=dtype)
+    wt = torch.empty(cin_pad, KH, KW, O, device=w.device, dtype=dtype) if with_t else None
+    w = w.detach().float().contiguous()
+    rec = np.zeros(1, _DESC)
+    rec[0] = (w.data_ptr(), wp.data_ptr(), wt.data_ptr() if wt is not None else 0, O, I, cin_pad, KH, KW, Kpad, 0,
+              O * Kpad)
+    d = torch.from_numpy(rec.view(np.uint8).copy()).to(w.device)
+    call("pack_conv_weights", DTYPES[dtype], d, 1, O * Kpad, stream())
+    torch.cuda.current_stream().synchronize()   # `d` / `w` are temporaries
+    return wp, wt
+
+
+class _Act:
+    """An NHWC activation tensor of the trunk graph."""
+
+    def __init__(self, C, H, W, name):
+        self.C, self.H, self.W, self.name = C, H, W, name
+        self.t = None      # forward value
+        self.g = None      # gradient buffer
+        self.pending = None  # gradient contribution waiting for the producer's dgrad (residual)
+
+
+class _ConvOp:
+    def __init__(self, conv, bn, src, name):
+        self.conv, self.bn, self.src, self.name = conv, bn, src, name
+        self.cin = conv.in_channels
+        self.cin_pad = 4 if self.cin < 8 else self.cin
+        self.cout = conv.out_channels
+        self.k = conv.kernel_size[0]
+        self.stride = conv.stride[0]
+        self.pad = conv.padding[0]
+        self.H, self.W = src.H, src.W
+        self.Ho = (self.H + 2 * self.pad - self.k) // self.stride + 1
+        self.Wo = (self.W + 2 * self.pad - self.k) // self.stride + 1
+        self.out = _Act(self.cout, self.Ho, self.Wo, name + ".y")
+        self.needs_dgrad = True
+
+
+class _ActOp:
+    """out = relu?(bn(y) [+ res_act | + bn_res(y_res)])"""
+
+    def __init__(self, cop, relu, res_act=None, res_conv=None, name=""):
+        self.cop, self.relu, self.res_act, self.res_conv = cop, relu, res_act, res_conv
+        self.out = _Act(cop.cout, cop.Ho, cop.Wo, name)
+
+
+class _PoolOp:
+    def __init__(self, src, k, s, p, name):
+        self.src, self.k, self.s, self.p = src, k, s, p
+        Ho = (src.H + 2 * p - k) // s + 1
+        Wo = (src.W + 2 * p - k) // s + 1
+        self.out = _Act(src.C, Ho, Wo, name)
+
+
+class TrunkEngine:
+    """Executes an nn.Sequential trunk (ResNet50 children[:-1] or the z-CNN)."""
+
+    def __init__(self, seq, in_channels, kind="resnet50"):
+        self.seq = seq
+        self.kind = kind
+        self.in_channels = in_channels
+        self._shape = None
+        self.generation = 0
+        self._saved_gen = -1
+        self._pack_key = None
+
+    # ------------------------------------------------------------ graph build
+    def _build(self, H, W):
+        self.ops = []
+        self.convs = []
+        x = _Act(4 if self.in_channels < 8 else self.in_channels, H, W, "input")
+        self.input = x
+
+        def conv_bn(conv, bn, src, name):
+            op = _ConvOp(conv, bn, src, name)
+            self.ops.append(op)
+            self.convs.append(op)
+            return op
+
+        if self.kind == "resnet50":
+            s = self.seq
+            c = conv_bn(s[0], s[1], x, "stem")
+            c.needs_dgrad = False
+            a = _ActOp(c, True, name="stem.act")
+            self.ops.append(a)
+            p = _PoolOp(a.out, 3, 2, 1, "stem.pool")
+            self.ops.append(p)
+            cur = p.out
+            for li in range(4):
+                for bi, blk in enumerate(s[4 + li]):
+                    nm = f"layer{li + 1}.{bi}"
+                    c1 = conv_bn(blk.conv1, blk.bn1, cur, nm + ".conv1")
+                    a1 = _ActOp(c1, True, name=nm + ".a1"); self.ops.append(a1)
+                    c2 = conv_bn(blk.conv2, blk.bn2, a1.out, nm + ".conv2")
+                    a2 = _ActOp(c2, True, name=nm + ".a2"); self.ops.append(a2)
+                    c3 = conv_bn(blk.conv3, blk.bn3, a2.out, nm + ".conv3")
+                    if blk.downsample is not None:
+                        cd = conv_bn(blk.downsample[0], blk.downsample[1], cur, nm + ".down")
+                        o = _ActOp(c3, True, res_conv=cd, name=nm + ".out")
+                    else:
+                        o = _ActOp(c3, True, res_act=cur, name=nm + ".out")
+                    self.ops.append(o)
+                    cur = o.out
+            self.final = cur
+        elif self.kind == "zcnn":
+            s = self.seq
+            cur = x
+            for i in (0, 4, 8, 12):
+                c = conv_bn(s[i], s[i + 1], cur, f"z{i}")
+                if i == 0:
+                    c.needs_dgrad = False
+                a = _ActOp(c, True, name=f"z{i}.act"); self.ops.append(a)
+                mp = s[i + 3]
+                p = _PoolOp(a.out, mp.kernel_size, mp.stride, mp.padding, f"z{i}.pool"); self.ops.append(p)
+                cur = p.out
+            self.final = cur
+        else:
+            raise ValueError(self.kind)
+        self.feat_dim = self.final.C
+
+    # ------------------------------------------------------------ allocation
+    def prepare(self, B, H, W, dtype, device):
+        key = (B, H, W, dtype, device)
+        if self._shape == key:
+            return
+        if dtype not in DTYPES:
+            raise Pose6dError(f"unsupported trunk dtype {dtype}")
+        self._build(H, W)
+        self._shape = key
+        self.B, self.dtype, self.dt, self.device = B, dtype, DTYPES[dtype], device
+        e = lambda *s, dt=dtype: torch.empty(*s, device=device, dtype=dt)
+        f32 = lambda *s: torch.empty(*s, device=device, dtype=torch.float32)
+        self.input.t = e(B, H, W, self.input.C)
+        ws_w, ws_bn = 0, 0
+        for op in self.ops:
+            o = op.out
+            o.t = e(B, o.H, o.W, o.C)
+            o.g = e(B, o.H, o.W, o.C)
+            if isinstance(op, _ConvOp):
+                M = B * op.Ho * op.Wo
+                kp = op.k * op.k * op.cin_pad
+                bk = 32 if dtype == torch.bfloat16 else 16
+                op.Kpad = (kp + bk - 1) // bk * bk
+                op.wp = e(op.cout, op.Kpad)
+                op.wt = e(op.cin_pad, op.k, op.k, op.cout) if op.needs_dgrad else None
+                rows = query("conv_stats_rows", B, op.Ho, op.Wo, op.cout)
+                op.stats_rows = rows
+                op.stats = f32(rows, 2, op.cout)
+                op.scale, op.shift, op.mean, op.inv = (f32(op.cout) for _ in range(4))
+                ws_w = max(ws_w, query("conv2d_wgrad_workspace", self.dt, B, op.Ho, op.Wo, op.cin_pad, op.cout, op.k,
+                                       op.k))
+                ws_bn = max(ws_bn, (query("bn_bwd_workspace_rows", M) * 2 + 3) * op.cout)
+                op.dres = e(B, op.H, op.W, op.cin_pad) if op.needs_dgrad else None
+            elif isinstance(op, _ActOp):
+                op.dz = e(B, o.H, o.W, o.C) if (op.res_act is not None or op.res_conv is not None) else None
+            elif isinstance(op, _PoolOp):
+                op.argmax = torch.empty(B, o.H, o.W, o.C, device=device, dtype=torch.uint8)
+        self.ws_wgrad = f32(max(ws_w // 4, 1))
+        self.ws_bn = f32(max(ws_bn, 1))
+        self.feat = f32(B, self.feat_dim)
+        self.feat_grad_in = None
+        # weight packing descriptors (one launch for all convs)
+        self._desc_dev = None
+        self._pack_key = None
+        self._build_pack_table()
+
+    def _build_pack_table(self):
+        n = len(self.convs)
+        sz = query("pack_desc_size")
+        assert sz == 64, sz
+        rec = np.zeros(n, dtype=_DESC)
+        start = 0
+        for i, op in enumerate(self.convs):
+            w = op.conv.weight
+            rec[i] = (w.data_ptr(), op.wp.data_ptr(), op.wt.data_ptr() if op.wt is not None else 0, op.cout, op.cin,
+                      op.cin_pad, op.k, op.k, op.Kpad, start, op.cout * op.Kpad)
+            start += op.cout * op.Kpad
+        self._pack_total = start
+        self._desc_dev = torch.from_numpy(rec.view(np.uint8).copy()).to(self.device)
+        self._desc_ptrs = tuple(op.conv.weight.data_ptr() for op in self.convs)
+
+    def pack_weights(self, force=False):
+        """Re-pack the conv weights if the fp32 masters changed (optimizer step,
+        load_state_dict, .to()).  One kernel launch for all convs."""
+        ptrs = tuple(op.conv.weight.data_ptr() for op in self.convs)
+        if ptrs != self._desc_ptrs:
+            self._build_pack_table()
+        key = (ptrs, tuple(op.conv.weight._version for op in self.convs))
+        if force or key != self._pack_key:
+            call("pack_conv_weights", self.dt, self._desc_dev, len(self.convs), self._pack_total, stream())
+            self._pack_key = key
+
+    # ------------------------------------------------------------ forward
+    def forward(self, x, training, pack=True):
+        """x: (B, C, H, W) fp32 on device -> features (B, feat_dim) fp32 (engine buffer)."""
+        require_device(x)
+        B, C, H, W = x.shape
+        if C != self.in_channels:
+            raise Pose6dError(f"trunk expects {self.in_channels} input channels, got {C}")
+        self.prepare(B, H, W, self.dtype_req, x.device)
+        if pack:
+            self.pack_weights()
+        st = stream()
+        dt = self.dt
+        xf = x.detach()
+        if xf.dtype != torch.float32:
+            xf = xf.float()
+        xf = xf.contiguous()
+        call("nchw_to_nhwc", dt, xf, self.input.t, B, C, H, W, self.input.C, st)
+        for op in self.ops:
+            if isinstance(op, _ConvOp):
+                bias = op.conv.bias
+                call("conv2d_fwd", dt, op.src.t, op.wp, bias.detach() if bias is not None else None, op.out.t,
+                     op.stats if training else None, B, op.H, op.W, op.cin_pad, op.cout, op.k, op.k, op.stride,
+                     op.pad, op.Ho, op.Wo, st)
+                bn = op.bn
+                call("bn_finalize", op.stats, op.stats_rows, op.cout, B * op.Ho * op.Wo, bn.weight.detach(),
+                     bn.bias.detach(), bn.running_mean, bn.running_var, bn.num_batches_tracked,
+                     float(bn.momentum if bn.momentum is not None else 0.1), float(bn.eps), int(training),
+                     op.scale, op.shift, op.mean, op.inv, st)
+            elif isinstance(op, _ActOp):
+                c = op.cop
+                M = B * c.Ho * c.Wo
+                if op.res_conv is not None:
+                    r = op.res_conv
+                    call("bn_act_fwd", dt, c.out.t, c.scale, c.shift, r.out.t, r.scale, r.shift, int(op.relu),
+                         op.out.t, M, c.cout, st)
+                else:
+                    call("bn_act_fwd", dt, c.out.t, c.scale, c.shift, op.res_act.t if op.res_act else None, None,
+                         None, int(op.relu), op.out.t, M, c.cout, st)
+            else:
+                s = op.src
+                call("maxpool_fwd", dt, s.t, op.out.t, op.argmax, B, s.H, s.W, s.C, op.k, op.s, op.p, op.out.H,
+                     op.out.W, st)
+        f = self.final
+        call("avgpool_fwd", dt, f.t, self.feat, B, f.H * f.W, f.C, st)
+        self.generation += 1
+        self._saved_gen = self.generation if training else -1
+        return self.feat
+
+    # ------------------------------------------------------------ backward
+    def backward(self, dfeat, grad_of, accumulate=False, on_conv_done=None):
+        """dfeat: (B, feat_dim) fp32.  grad_of(param) -> fp32 tensor receiving that
+        parameter's gradient (written, or added if accumulate).  Input gets no grad."""
+        if self._saved_gen != self.generation:
+            raise Pose6dError("TrunkEngine.backward: activations of the matching training forward were overwritten")
+        st = stream()
+        dt = self.dt
+        B = self.B
+        acc = int(accumulate)
+        f = self.final
+        dfeat = dfeat.detach().float().contiguous()
+        call("avgpool_bwd", dt, dfeat, f.g, B, f.H * f.W, f.C, st)
+        for op in self.ops:
+            op.out.pending = None
+        self.input.pending = None
+        for op in reversed(self.ops):
+            if isinstance(op, _ActOp):
+                c = op.cop
+                M = B * c.Ho * c.Wo
+                bn = c.bn
+                call("bn_bwd", dt, op.out.g, op.out.t if op.relu else None, c.out.t, c.mean, c.inv,
+                     bn.weight.detach(), grad_of(bn.weight), grad_of(bn.bias), acc, c.out.g, op.dz, self.ws_bn, M,
+                     c.cout, st)
+                if op.res_conv is not None:
+                    r = op.res_conv
+                    # identity branch = bn_r(y_r) (no ReLU of its own): its dz is the masked dout
+                    call("bn_bwd", dt, op.dz, None, r.out.t, r.mean, r.inv, r.bn.weight.detach(),
+                         grad_of(r.bn.weight), grad_of(r.bn.bias), acc, r.out.g, None, self.ws_bn, M, r.cout, st)
+                elif op.res_act is not None:
+                    op.res_act.pending = op.dz
+            elif isinstance(op, _ConvOp):
+                dy = op.out.g
+                M = B * op.Ho * op.Wo
+                call("conv2d_wgrad", dt, op.src.t, dy, grad_of(op.conv.weight), acc, self.ws_wgrad, B, op.H, op.W,
+                     op.cin_pad, op.cin, op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, st)
+                if op.conv.bias is not None:
+                    call("channel_sum", dt, dy, M, op.cout, grad_of(op.conv.bias), acc, st)
+                if op.needs_dgrad:
+                    src = op.src
+                    if src.pending is not None and src.g is not None and src.pending is not src.g:
+                        # a residual contribution is waiting: fuse it into this dgrad's epilogue
+                        call("conv2d_dgrad", dt, dy, op.wt, src.pending, src.g, B, op.H, op.W, op.cin_pad, op.cout,
+                             op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, st)
+                        src.pending = None
+                    elif src.pending is None and self._has_later_consumer(op):
+                        # first of two contributions (downsample branch): park it in dres
+                        call("conv2d_dgrad", dt, dy, op.wt, None, op.dres, B, op.H, op.W, op.cin_pad, op.cout, op.k,
+                             op.k, op.stride, op.pad, op.Ho, op.Wo, st)
+                        src.pending = op.dres
+                    else:
+                        call("conv2d_dgrad", dt, dy, op.wt, None, src.g, B, op.H, op.W, op.cin_pad, op.cout, op.k,
+                             op.k, op.stride, op.pad, op.Ho, op.Wo, st)
+                if on_conv_done is not None:
+                    on_conv_done(op)
+            else:
+                s = op.src
+                call("maxpool_bwd", dt, op.out.g, op.argmax, s.g, B, s.H, s.W, s.C, op.k, op.s, op.p, op.out.H,
+                     op.out.W, st)
+
+    def _has_later_consumer(self, op):
+        """True if op.src is also consumed by a conv processed later in backward
+        (i.e. earlier in forward): the downsample conv of a block shares its input
+        with the block's conv1."""
+        idx = self.ops.index(op)
+        for prev in self.ops[:idx]:
+            if isinstance(prev, _ConvOp) and prev.src is op.src and prev.needs_dgrad:
+                return True
+        return False
+
+    dtype_req = torch.float32
+
+    def set_dtype(self, dtype):
+        self.dtype_req = dtype
+
+    def params_in_grad_order(self):
+        """Parameters in the order backward() finishes their gradients."""
+        out = []
+        for op in reversed(self.ops):
+            if isinstance(op, _ActOp):
+                out += [op.cop.bn.weight, op.cop.bn.bias]
+                if op.res_conv is not None:
+                    out += [op.res_conv.bn.weight, op.res_conv.bn.bias]
+            elif isinstance(op, _ConvOp):
+                out.append(op.conv.weight)
+                if op.conv.bias is not None:
+                    out.append(op.conv.bias)
+        return out

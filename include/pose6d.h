@@ -155,6 +155,10 @@ int pose6d_bn_bwd(int32_t dtype, const void *dout, const void *out, const void *
                   const float *invstd, const float *gamma, float *dgamma, float *dbeta, int32_t accumulate, void *dy,
                   void *dz_out, float *workspace, int64_t M, int32_t C, void *stream);
 
+/* conv bias gradient: out[c] (+)= sum_m x[m][c] over an NHWC tensor of M pixels */
+int pose6d_channel_sum(int32_t dtype, const void *x, int64_t M, int32_t C, float *out, int32_t accumulate,
+                       void *stream);
+
 /* nn.MaxPool2d(k, s, p) on NHWC; argmax = window index (uint8) of the first max */
 int pose6d_maxpool_fwd(int32_t dtype, const void *x, void *y, uint8_t *argmax, int32_t N, int32_t H, int32_t W,
                        int32_t C, int32_t k, int32_t s, int32_t p, int32_t Ho, int32_t Wo, void *stream);
@@ -174,17 +178,18 @@ int pose6d_gemm_f32(const float *A, int64_t sam, int64_t sak, const float *B, in
                     int64_t ldc, const float *bias, int32_t M, int32_t N, int32_t K, float alpha, float beta,
                     void *stream);
 int pose6d_colsum_f32(const float *dy, float *db, int32_t M, int32_t N, int32_t accumulate, void *stream);
-/* BatchNorm1d (+ReLU) (+Dropout p_drop with a counter-based RNG keyed by seed) */
+/* BatchNorm1d (+ReLU) (+Dropout p_drop with a counter-based RNG keyed by the
+ * device word *seed xor salt -- a device word so graph replays draw new masks) */
 int pose6d_bn1d_fwd(const float *x, float *y, int32_t M, int32_t C, const float *gamma, const float *beta,
                     float *running_mean, float *running_var, int64_t *num_batches, float momentum, float eps,
-                    int32_t training, int32_t relu, float p_drop, uint64_t seed, uint8_t *mask, float *save_mean,
-                    float *save_invstd, void *stream);
+                    int32_t training, int32_t relu, float p_drop, const uint64_t *seed, uint64_t salt, uint8_t *mask,
+                    float *save_mean, float *save_invstd, void *stream);
 int pose6d_bn1d_bwd(const float *dy, const float *x, const float *y, int32_t M, int32_t C, const float *gamma,
                     const float *save_mean, const float *save_invstd, int32_t training, int32_t relu, float p_drop,
                     const uint8_t *mask, float *dx, float *dgamma, float *dbeta, int32_t accumulate, void *stream);
 /* act: 0 identity, 1 ReLU, 2 GELU (erf); optional dropout */
-int pose6d_act_fwd(const float *x, float *y, int64_t n, int32_t act, float p_drop, uint64_t seed, uint8_t *mask,
-                   void *stream);
+int pose6d_act_fwd(const float *x, float *y, int64_t n, int32_t act, float p_drop, const uint64_t *seed,
+                   uint64_t salt, uint8_t *mask, void *stream);
 int pose6d_act_bwd(const float *dy, const float *x, float *dx, int64_t n, int32_t act, float p_drop,
                    const uint8_t *mask, void *stream);
 

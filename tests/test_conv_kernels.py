@@ -1,0 +1,173 @@
+"""Per-kernel numerics of the conv / BN / pool kernels through the C ABI, against a
+plain torch-CPU fp32 reference of the same op (fp32 kernels: 1e-4 relative;
+bf16 kernels: against the fp32 op on bf16-rounded operands, bf16 tolerance)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+CONFIGS = [
+    # N, H, W, Cin, Cout, k, s, p, bias
+    (2, 14, 14, 64, 128, 1, 1, 0, False),    # 1x1 (GEMM mode), M not a tile multiple
+    (2, 28, 28, 256, 512, 1, 2, 0, False),   # downsample 1x1/s2
+    (2, 14, 14, 64, 64, 3, 1, 1, False),     # bottleneck 3x3
+    (2, 28, 28, 128, 128, 3, 2, 1, False),   # stride-2 3x3
+    (2, 32, 32, 3, 64, 7, 2, 3, False),      # stem 7x7/s2, Cin 3 padded to 4
+    (2, 16, 16, 32, 64, 5, 1, 2, True),      # z-CNN 5x5 (+bias)
+    (2, 32, 32, 3, 32, 7, 2, 3, True),       # z-CNN stem, Cout 32 (+bias)
+    (1, 7, 7, 512, 2048, 1, 1, 0, False),    # layer4 expand
+]
+
+
+def _close(got, ref, rtol, what):
+    got = got.float().cpu()
+    ref = ref.float().cpu()
+    scale = ref.abs().max().item() + 1e-30
+    err = (got - ref).abs()
+    bad = err > (rtol * ref.abs() + rtol * scale)
+    assert not bool(bad.any()), f"{what}: max err {err.max().item():.3e} (scale {scale:.3e}), {int(bad.sum())} bad"
+
+
+def _nhwc(t, cpad=None):
+    t = t.permute(0, 2, 3, 1).contiguous()
+    if cpad is not None and cpad > t.shape[-1]:
+        t = F.pad(t, (0, cpad - t.shape[-1]))
+    return t
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_conv_fwd_dgrad_wgrad(cfg, dtype):
+    from pose6d._lib import call, query, stream
+    from pose6d.trunk import DTYPES, pack_single
+    N, H, W, Cin, Cout, k, s, p, has_bias = cfg
+    g = torch.Generator().manual_seed(hash(cfg) & 0xFFFF)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, k, k, generator=g) * (2.0 / (Cin * k * k)) ** 0.5
+    b = torch.randn(Cout, generator=g) if has_bias else None
+    if dtype == torch.bfloat16:   # the reference sees the same rounded operands
+        x = x.bfloat16().float()
+        w = w.bfloat16().float()
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    cpad = 4 if Cin < 8 else Cin
+    dt = DTYPES[dtype]
+    dev = "cuda"
+    xd = _nhwc(x, cpad).to(dev, dtype)
+    wd = w.to(dev)
+    wp, wt = pack_single(wd, cpad, dtype, with_t=Cin >= 8)
+    y = torch.empty(N, Ho, Wo, Cout, device=dev, dtype=dtype)
+    rows = query("conv_stats_rows", N, Ho, Wo, Cout)
+    stats = torch.empty(rows, 2, Cout, device=dev)
+    call("conv2d_fwd", dt, xd, wp, b.to(dev) if b is not None else None, y, stats, N, H, W, cpad, Cout, k, k, s, p,
+         Ho, Wo, stream())
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yr = F.conv2d(xr, wr, b, stride=s, padding=p)
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    _close(y.permute(0, 3, 1, 2), yr.detach(), tol, "fwd")
+    st = stats.sum(0).cpu()
+    _close(st[0], yr.detach().sum((0, 2, 3)), 1e-4 if dtype == torch.float32 else 1e-2, "stats.sum")
+    _close(st[1], (yr.detach() ** 2).sum((0, 2, 3)), 1e-4 if dtype == torch.float32 else 1e-2, "stats.sumsq")
+
+    dy = torch.randn(N, Cout, Ho, Wo, generator=g)
+    if dtype == torch.bfloat16:
+        dy = dy.bfloat16().float()
+    yr.backward(dy)
+    dyd = _nhwc(dy).to(dev, dtype)
+    if Cin >= 8:
+        dres = torch.randn(N, H, W, Cin, generator=g).to(dev, dtype)
+        dx = torch.empty(N, H, W, Cin, device=dev, dtype=dtype)
+        call("conv2d_dgrad", dt, dyd, wt, dres, dx, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream())
+        _close(dx.permute(0, 3, 1, 2), xr.grad + dres.float().cpu().permute(0, 3, 1, 2), tol, "dgrad(+res)")
+    ws = torch.empty(query("conv2d_wgrad_workspace", dt, N, Ho, Wo, cpad, Cout, k, k) // 4 + 1, device=dev)
+    dw = torch.full((Cout, Cin, k, k), 7.0, device=dev)
+    call("conv2d_wgrad", dt, xd, dyd, dw, 0, ws, N, H, W, cpad, Cin, Cout, k, k, s, p, Ho, Wo, stream())
+    _close(dw, wr.grad, tol, "wgrad")
+    dw2 = dw.clone()
+    call("conv2d_wgrad", dt, xd, dyd, dw2, 1, ws, N, H, W, cpad, Cin, Cout, k, k, s, p, Ho, Wo, stream())
+    _close(dw2, 2 * wr.grad, tol, "wgrad accumulate")
+    if has_bias:
+        db = torch.empty(Cout, device=dev)
+        call("channel_sum", dt, dyd, N * Ho * Wo, Cout, db, 0, stream())
+        _close(db, dy.sum((0, 2, 3)), tol, "bias grad")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bn_act_and_backward(dtype):
+    from pose6d._lib import call, query, stream
+    from pose6d.trunk import DTYPES
+    g = torch.Generator().manual_seed(3)
+    N, H, W, C = 4, 9, 9, 64
+    M = N * H * W
+    y = torch.randn(N, C, H, W, generator=g) * 2 + 0.5
+    res = torch.randn(N, C, H, W, generator=g)
+    if dtype == torch.bfloat16:
+        y, res = y.bfloat16().float(), res.bfloat16().float()
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g)
+    dev, dt = "cuda", DTYPES[dtype]
+    # statistics partials as the conv epilogue would emit them (one row)
+    stats = torch.stack([y.sum((0, 2, 3)), (y * y).sum((0, 2, 3))]).reshape(1, 2, C).to(dev)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    nbt = torch.zeros((), dtype=torch.long, device=dev)
+    sc, sh, mu, iv = (torch.empty(C, device=dev) for _ in range(4))
+    call("bn_finalize", stats, 1, C, M, gamma.to(dev), beta.to(dev), rm, rv, nbt, 0.1, 1e-5, 1, sc, sh, mu, iv, stream())
+    yd, rd = _nhwc(y).to(dev, dtype), _nhwc(res).to(dev, dtype)
+    out = torch.empty_like(yd)
+    call("bn_act_fwd", dt, yd, sc, sh, rd, None, None, 1, out, M, C, stream())
+    yr = y.clone().requires_grad_(True)
+    rrm, rrv = torch.zeros(C), torch.ones(C)
+    o_ref = F.relu(F.batch_norm(yr, rrm, rrv, gamma, beta, True, 0.1, 1e-5) + res)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    _close(out.permute(0, 3, 1, 2), o_ref.detach(), tol * 10, "bn_act")
+    _close(rm, rrm, 1e-5, "running_mean")
+    _close(rv, rrv, 1e-5, "running_var")
+    assert int(nbt.item()) == 1
+    dout = torch.randn(N, C, H, W, generator=g)
+    if dtype == torch.bfloat16:
+        dout = dout.bfloat16().float()
+    o_ref.backward(dout)
+    ws = torch.empty((query("bn_bwd_workspace_rows", M) * 2 + 3) * C, device=dev)
+    dy = torch.empty_like(yd)
+    dz = torch.empty_like(yd)
+    dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    call("bn_bwd", dt, _nhwc(dout).to(dev, dtype), out, yd, mu, iv, gamma.to(dev), dg, db, 0, dy, dz, ws, M, C,
+         stream())
+    _close(dy.permute(0, 3, 1, 2), yr.grad, 1e-4 if dtype == torch.float32 else 3e-2, "bn dy")
+    mask = (o_ref.detach() > 0).float()
+    _close(dz.permute(0, 3, 1, 2), dout * mask, 1e-6, "dz")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_pools(dtype):
+    from pose6d._lib import call, stream
+    from pose6d.trunk import DTYPES
+    g = torch.Generator().manual_seed(4)
+    dev, dt = "cuda", DTYPES[dtype]
+    for (N, H, W, C, k, s, p) in [(2, 16, 16, 64, 3, 2, 1), (2, 14, 14, 32, 2, 2, 0)]:
+        x = torch.randn(N, C, H, W, generator=g)
+        x = F.relu(x)                         # many exact ties (zeros), as after ReLU
+        if dtype == torch.bfloat16:
+            x = x.bfloat16().float()
+        Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        xd = _nhwc(x).to(dev, dtype)
+        y = torch.empty(N, Ho, Wo, C, device=dev, dtype=dtype)
+        am = torch.empty(N, Ho, Wo, C, device=dev, dtype=torch.uint8)
+        call("maxpool_fwd", dt, xd, y, am, N, H, W, C, k, s, p, Ho, Wo, stream())
+        xr = x.clone().requires_grad_(True)
+        yr = F.max_pool2d(xr, k, s, p)
+        assert torch.equal(y.float().cpu().permute(0, 3, 1, 2), yr.detach())
+        dy = torch.randn(N, C, Ho, Wo, generator=g)
+        if dtype == torch.bfloat16:
+            dy = dy.bfloat16().float()
+        yr.backward(dy)
+        dx = torch.empty_like(xd)
+        call("maxpool_bwd", dt, _nhwc(dy).to(dev, dtype), am, dx, N, H, W, C, k, s, p, Ho, Wo, stream())
+        _close(dx.permute(0, 3, 1, 2), xr.grad, 1e-6 if dtype == torch.float32 else 1e-2, "maxpool bwd")
+    x = torch.randn(2, 64, 7, 7, generator=g)
+    f = torch.empty(2, 64, device=dev)
+    call("avgpool_fwd", 0, _nhwc(x).to(dev), f, 2, 49, 64, stream())
+    _close(f, x.mean((2, 3)), 1e-6, "avgpool")
