@@ -398,3 +398,14 @@ extern "C" int pose6d_conv2d_dgrad(int32_t dtype, const void* dy, const void* wt
   return dtype == POSE6D_DT_BF16 ? dispatch<bf16>(mode, g, tile, dy, wt, nullptr, dres, dx, nullptr, s)
                                  : dispatch<float>(mode, g, tile, dy, wt, nullptr, dres, dx, nullptr, s);
 }
+
+// launch variant of a forward / data-gradient conv: (mode << 4) | tile, with tile
+// 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64 (for profiling / roofline joins)
+extern "C" int pose6d_conv_variant(int32_t pass, int32_t M, int32_t Ncols, int32_t KH, int32_t KW, int32_t stride,
+                                   int32_t pad, int32_t Cin) {
+  int mode;
+  if (KH == 1 && KW == 1 && stride == 1 && pad == 0) mode = kGemm;
+  else if (pass == 0) mode = Cin == 4 ? kFwdNarrow : kFwd;
+  else mode = kDgrad;
+  return (mode << 4) | pick_tile(M, Ncols);
+}

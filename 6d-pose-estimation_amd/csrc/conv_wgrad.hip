@@ -319,3 +319,10 @@ extern "C" int pose6d_conv2d_wgrad(int32_t dtype, const void* x, const void* dy,
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
+
+// tile of the weight-gradient kernel: (BM == 128) << 1 | (BN == 128)
+extern "C" int pose6d_wgrad_variant(int32_t dtype, int32_t M, int32_t Cout, int32_t K) {
+  const int bk = dtype == POSE6D_DT_BF16 ? 32 : 16;
+  const Plan p = plan(M, Cout, p6::ceil_div(K, bk) * bk);
+  return ((p.bm == 128) << 1) | (p.bn == 128);
+}

@@ -8,7 +8,7 @@
 //                          clip coefficient min(1, max_norm/(norm+1e-6)); AdamW
 //                          update in torch's operation order.
 // Hyper-parameters come from a device array (graph replays pick up lr changes):
-//   hp = {lr, beta1, beta2, eps, weight_decay, bias_correction1, bias_correction2, max_norm}
+//   hp = {lr, beta1, beta2, eps, weight_decay, step (t >= 1), unused, max_norm}
 #include "common.h"
 
 namespace {
@@ -39,7 +39,11 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float* __restrict__ p, 
                                                          const float* __restrict__ hp, float* __restrict__ norm_out) {
   __shared__ float s_coef;
   __shared__ double red[kThreads / 64];
-  const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4], bc1 = hp[5], bc2 = hp[6], max_norm = hp[7];
+  const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4], max_norm = hp[7];
+  // bias corrections from the device step counter hp[5] (incremented in-stream, so
+  // a captured step replays with the right t): 1 - beta^t as torch computes it
+  const double t = (double)hp[5];
+  const float bc1 = (float)(1.0 - pow((double)b1, t)), bc2 = (float)(1.0 - pow((double)b2, t));
   if (max_norm > 0.f) {
     double s = 0.0;
     for (int i = threadIdx.x; i < nparts; i += kThreads) s += (double)part[i];

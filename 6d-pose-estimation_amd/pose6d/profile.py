@@ -1,0 +1,78 @@
+"""Per-kernel timing of a TrunkEngine's convolutions with HIP events (on the stream
+the kernels are launched on), grouped by kernel symbol so the averages line up
+with rocprofv3 --kernel-trace --stats rows."""
+import collections
+
+import torch
+
+from ._lib import call, query, stream
+
+TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}
+
+
+def _tname(dtype):
+    return "__bf16" if dtype == torch.bfloat16 else "float"
+
+
+def conv_launches(eng):
+    """(symbol, flops, launch-callable) for every conv pass of one training step."""
+    B, dt, T = eng.B, eng.dt, _tname(eng.dtype)
+    st = stream()
+    out = []
+    for op in eng.convs:
+        M = B * op.Ho * op.Wo
+        K = op.k * op.k * op.cin
+        flops = 2.0 * M * op.cout * K
+        v = query("conv_variant", 0, M, op.cout, op.k, op.k, op.stride, op.pad, op.cin_pad)
+        bm, bn = TILES[v & 15]
+        sym = f"conv_igemm_kernel<{T}, {bm}, {bn}, {v >> 4}>"
+
+        def fwd(op=op):
+            call("conv2d_fwd", dt, op.src.t, op.wp, op.conv.bias, op.out.t, op.stats, B, op.H, op.W, op.cin_pad,
+                 op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, st)
+        out.append((sym, flops, fwd, op.name + ".fwd"))
+        if op.needs_dgrad:
+            Md = B * op.H * op.W
+            v = query("conv_variant", 1, Md, op.cin_pad, op.k, op.k, op.stride, op.pad, op.cin_pad)
+            bm, bn = TILES[v & 15]
+            sym = f"conv_igemm_kernel<{T}, {bm}, {bn}, {v >> 4}>"
+
+            def dgrad(op=op):
+                call("conv2d_dgrad", dt, op.out.g, op.wt, None, op.dres, B, op.H, op.W, op.cin_pad, op.cout, op.k,
+                     op.k, op.stride, op.pad, op.Ho, op.Wo, st)
+            out.append((sym, flops, dgrad, op.name + ".dgrad"))
+        v = query("wgrad_variant", dt, M, op.cout, op.k * op.k * op.cin_pad)
+        sym = f"conv_wgrad_kernel<{T}, {128 if v & 2 else 64}, {128 if v & 1 else 64}>"
+        dw = torch.empty_like(op.conv.weight)
+
+        def wgrad(op=op, dw=dw):
+            call("conv2d_wgrad", dt, op.src.t, op.out.g, dw, 0, eng.ws_wgrad, B, op.H, op.W, op.cin_pad, op.cin,
+                 op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, st)
+        out.append((sym + "+reduce", flops, wgrad, op.name + ".wgrad"))
+    return out
+
+
+def time_launches(launches, reps=10):
+    """Average duration of each launch (events bracket `reps` back-to-back launches)."""
+    res = []
+    s = torch.cuda.current_stream()
+    for sym, flops, fn, name in launches:
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            fn()
+        e1.record(s)
+        e1.synchronize()
+        res.append((sym, flops, e0.elapsed_time(e1) / reps * 1e-3, name))
+    return res
+
+
+def by_symbol(timed):
+    agg = collections.OrderedDict()
+    for sym, flops, t, name in timed:
+        a = agg.setdefault(sym, {"launches": 0, "time_s": 0.0, "flops": 0.0})
+        a["launches"] += 1
+        a["time_s"] += t
+        a["flops"] += flops
+    return agg

@@ -1,0 +1,238 @@
+"""Whole-step trainer for the north-star workload: PoseNetRGBDGeometric training
+(forward + PoseLoss(1, 10, geodesic) + backward + clip_grad_norm_(1.0) + AdamW),
+i.e. the per-batch body of the reference's train() loop
+(scripts/training/train_rgbd_geometric.py:97-115), without autograd or host syncs.
+
+MI355X design:
+  * one flat fp32 arena for parameters / gradients / AdamW moments (the module's
+    Parameters become views into it: state_dict, checkpoints, torch optimizers
+    keep working), parameters laid out in gradient-completion order so that DDP
+    buckets are contiguous prefixes that become ready one after another;
+  * the entire step (~400 launches) is captured once into a hipGraph and
+    replayed; the AdamW step counter, dropout seed and lr live in device memory
+    so replays stay exact;
+  * data parallel: one process per GPU, batch shards, gradient all-reduce over
+    RCCL (torch.distributed 'nccl'); bucketed all-reduces are issued on a comm
+    stream as soon as each bucket's gradients exist, overlapping the rest of the
+    backward (replay is split at bucket boundaries for that).
+"""
+import math
+
+import torch
+
+from ._lib import call, stream
+from .head import HeadEngine
+from .trunk import TrunkEngine
+
+NPART = 1024
+
+
+class FlatArena:
+    """Parameters (in the given order) re-homed into one flat fp32 buffer."""
+
+    def __init__(self, params, device, align=64):
+        self.params = list(params)
+        self.offsets = []
+        off = 0
+        for p in self.params:
+            self.offsets.append(off)
+            off += (p.numel() + align - 1) // align * align
+        self.numel = off
+        self.flat = torch.zeros(off, device=device, dtype=torch.float32)
+        self.grad = torch.zeros(off, device=device, dtype=torch.float32)
+        self._views = {}
+        with torch.no_grad():
+            for p, o in zip(self.params, self.offsets):
+                v = self.flat[o:o + p.numel()].view_as(p)
+                v.copy_(p.data)
+                p.data = v
+                self._views[id(p)] = self.grad[o:o + p.numel()].view_as(p)
+
+    def grad_of(self, p):
+        return self._views[id(p)]
+
+    def end_offset(self, p):
+        if not hasattr(self, "_index"):
+            self._index = {id(q): i for i, q in enumerate(self.params)}
+        i = self._index[id(p)]
+        return self.offsets[i] + self.params[i].numel()
+
+
+class RGBDGeometricTrainer:
+    """Fused, graph-captured training step for PoseNetRGBDGeometric."""
+
+    def __init__(self, model, batch, dtype=torch.bfloat16, lr=1e-4, weight_decay=1e-4, max_norm=1.0,
+                 betas=(0.9, 0.999), eps=1e-8, rot_weight=1.0, trans_weight=10.0, process_group=None,
+                 bucket_mb=25.0):
+        self.model = model
+        self.B = batch
+        dev = next(model.parameters()).device
+        self.dev = dev
+        model.train()
+        self.trunk = TrunkEngine(model.backbone, 3)
+        self.trunk.set_dtype(dtype)
+        self.head = HeadEngine(model.rot_head)
+        order = self.head.params_in_grad_order() + self.trunk.params_in_grad_order()
+        assert len(order) == len(list(model.parameters())) and {id(p) for p in order} == \
+            {id(p) for p in model.parameters()}
+        self.arena = FlatArena(order, dev)
+        self.m = torch.zeros_like(self.arena.flat)
+        self.v = torch.zeros_like(self.arena.flat)
+        self.hp = torch.tensor([lr, betas[0], betas[1], eps, weight_decay, 0.0, 0.0, max_norm], device=dev,
+                               dtype=torch.float32)
+        self.partials = torch.zeros(NPART, device=dev)
+        self.norm = torch.zeros(1, device=dev)
+        self.loss = torch.zeros((), device=dev)
+        self.rot = torch.empty(batch, 4, device=dev)
+        self.trans = torch.empty(batch, 3, device=dev)
+        self.drot = torch.empty(batch, 4, device=dev)
+        self.dtrans = torch.empty(batch, 3, device=dev)
+        self.draw = torch.empty(batch, 4, device=dev)
+        self.one = torch.ones((), device=dev)
+        self.seed = torch.tensor([torch.initial_seed() & 0x7FFFFFFFFFFF], device=dev, dtype=torch.int64)
+        self.wr, self.wt = float(rot_weight), float(trans_weight)
+        self.pg = process_group
+        self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        self.graphs = None
+        self._buckets(bucket_mb)
+
+    # ------------------------------------------------------------- DDP buckets
+    def _buckets(self, bucket_mb):
+        """Split the flat gradient into contiguous buckets; each closes after the
+        backward of the conv whose weight is its last parameter."""
+        self.bucket_ends = []
+        if self.world == 1:
+            return
+        limit = int(bucket_mb * 1e6 / 4)
+        start = 0
+        for p, off in zip(self.arena.params, self.arena.offsets):
+            end = off + p.numel()
+            if end - start >= limit:
+                self.bucket_ends.append((p, end))
+                start = end
+        if not self.bucket_ends or self.bucket_ends[-1][1] != self.arena.numel:
+            self.bucket_ends.append((self.arena.params[-1], self.arena.numel))
+
+    # ------------------------------------------------------------- the step
+    def _forward_loss(self, rgb, depth_raw, bbox, K, gt_rot, gt_trans):
+        st = stream()
+        feat = self.trunk.forward(rgb, True, pack=False)
+        raw = self.head.forward(feat, True, seed_dev=self.seed, salt=1)
+        call("rownorm_fwd", raw, self.rot, self.B, 4, 0, st)
+        call("pinhole_depth", depth_raw, depth_raw.shape[1], depth_raw.shape[2], bbox, K, 1 if K.dim() == 3 else 0,
+             self.B, self.trans, st)
+        call("pose_loss_fwd", self.rot, self.trans, gt_rot, gt_trans, self.B, self.wr, self.wt, 0, self.loss, st)
+        call("pose_loss_bwd", self.rot, self.trans, gt_rot, gt_trans, self.B, self.wr, self.wt, 0, self.one,
+             self.drot, self.dtrans, st)
+        call("rownorm_bwd", raw, self.drot, self.draw, self.B, 4, 0, st)
+        return raw
+
+    def _head_backward(self):
+        return self.head.backward(self.draw, self.arena.grad_of)
+
+    def _optimizer(self):
+        st = stream()
+        if self.world > 1:
+            self.arena.grad.mul_(1.0 / self.world)
+        self.hp[5:6].add_(1.0)
+        call("sumsq_partial", self.arena.grad, self.arena.numel, self.partials, NPART, st)
+        call("adamw_step", self.arena.flat, self.arena.grad, self.m, self.v, self.arena.numel, self.partials, NPART,
+             self.hp, self.norm, st)
+        self.seed.add_(1)
+
+    def step_eager(self, data):
+        """One training step without graphs (reference order of operations)."""
+        self.trunk.pack_weights(force=True)
+        self._forward_loss(*data)
+        dfeat = self._head_backward()
+        if self.world == 1:
+            self.trunk.backward(dfeat, self.arena.grad_of)
+        else:
+            self._backward_ddp(dfeat)
+        self._optimizer()
+
+    # ------------------------------------------------------------- DDP backward
+    def _backward_ddp(self, dfeat):
+        """Trunk backward with bucketed all-reduce: when the conv that completes a
+        bucket is done, the bucket's all-reduce is enqueued on the comm stream
+        (ordered after that point by an event) and overlaps the rest of backward."""
+        import torch.distributed as dist
+        comm = self._comm_stream()
+        handles = []
+        state = {"start": 0, "next": 0}
+        cur = torch.cuda.current_stream()
+
+        def issue_upto(done):
+            # every bucket whose end lies within the completed prefix [0, done)
+            while state["next"] < len(self.bucket_ends) and self.bucket_ends[state["next"]][1] <= done:
+                end = self.bucket_ends[state["next"]][1]
+                s = state["start"]
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                with torch.cuda.stream(comm):
+                    comm.wait_event(ev)
+                    handles.append(dist.all_reduce(self.arena.grad[s:end], group=self.pg, async_op=True))
+                state["start"] = end
+                state["next"] += 1
+
+        def on_conv(op):
+            # gradients complete in arena order: after this conv, everything up to its
+            # last parameter (weight, or bias if it has one) is final
+            last = op.conv.bias if op.conv.bias is not None else op.conv.weight
+            issue_upto(self.arena.end_offset(last))
+
+        self.trunk.backward(dfeat, self.arena.grad_of, on_conv_done=on_conv)
+        issue_upto(self.arena.numel)
+        for h in handles:
+            h.wait()
+        cur.wait_stream(comm)
+
+    def _comm_stream(self):
+        if not hasattr(self, "_comm"):
+            self._comm = torch.cuda.Stream(device=self.dev)
+        return self._comm
+
+    # ------------------------------------------------------------- graphs
+    def capture(self, data, warmup=2):
+        """Capture the step (world == 1: one graph; world > 1: forward+head graph,
+        eager bucketed backward, optimizer graph)."""
+        s = torch.cuda.Stream(device=self.dev)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.step_eager(data)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        if self.world == 1:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.trunk.pack_weights(force=True)
+                self._forward_loss(*data)
+                dfeat = self._head_backward()
+                self.trunk.backward(dfeat, self.arena.grad_of)
+                self._optimizer()
+            self.graphs = [g]
+        else:
+            g1 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1):
+                self.trunk.pack_weights(force=True)
+                self._forward_loss(*data)
+                self._dfeat = self._head_backward()
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2):
+                self._optimizer()
+            self.graphs = [g1, g2]
+        torch.cuda.synchronize()
+
+    def step(self, data=None):
+        if self.graphs is None:
+            return self.step_eager(data)
+        if self.world == 1:
+            self.graphs[0].replay()
+        else:
+            self.graphs[0].replay()
+            self._backward_ddp(self._dfeat)
+            self.graphs[1].replay()
+
+    def set_lr(self, lr):
+        self.hp[0].fill_(lr)

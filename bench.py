@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Benchmark: crops/s of PoseNetRGBDGeometric training at batch 32 x 224^2 per GPU
+(BASELINE.json metric; config 3 on one GPU, config 5 = the same per rank over
+N GPUs).  A step = forward + PoseLoss(1, 10, geodesic) + backward +
+clip_grad_norm_(1.0) + AdamW, the body of train_rgbd_geometric.py:97-115, on
+synthetic device-resident inputs of the reference's shapes, bf16 trunk.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+Prints ONE JSON line on rank 0 (contract in the task statement), including
+"roofline" for the dominant kernel (HIP events, grouped by kernel symbol) and
+"cpu_baseline" (the oracle's torch-CPU fp32 restatement of the same step,
+rank 0 only, bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+import warnings
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [REPO, os.path.join(REPO, "6d-pose-estimation_amd")]
+warnings.simplefilter("ignore")
+
+import torch  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0       # HBM3E spec
+FWD_BYTES_PER_CROP = 58.45e6   # bf16 fused-ideal forward bytes / crop
+
+
+def synth_batch(B, dev, seed):
+    """SURVEY.md §8(d) synthetic inputs (seeded), resident on the device."""
+    g = torch.Generator().manual_seed(seed)
+    rgb = torch.randn(B, 3, 224, 224, generator=g)
+    depth_raw = torch.rand(B, 224, 224, generator=g) * 1.3 + 0.3
+    depth_raw[torch.rand(B, 224, 224, generator=g) < 0.05] = 0.0
+    bbox = torch.rand(B, 2, generator=g) * 223
+    s = 224.0 / (torch.rand(B, generator=g) * 200 + 100)
+    K = torch.zeros(B, 3, 3)
+    K[:, 0, 0] = K[:, 1, 1] = 572.4 * s
+    K[:, 0, 2] = torch.rand(B, generator=g) * 224
+    K[:, 1, 2] = torch.rand(B, generator=g) * 224
+    K[:, 2, 2] = 1.0
+    gt_rot = torch.nn.functional.normalize(torch.randn(B, 4, generator=g), dim=1)
+    gt_trans = torch.randn(B, 3, generator=g) * 0.1 + torch.tensor([0.0, 0.0, 0.8])
+    return [t.to(dev).contiguous() for t in (rgb, depth_raw, bbox, K, gt_rot, gt_trans)]
+
+
+def cpu_baseline(batch=32, steps=2, threads=None):
+    """The oracle (torch-CPU fp32 restatement, shown equal to the reference on the
+    golden fixtures) doing the same training step on the host cores."""
+    from oracle import pose_loss as OP
+    from oracle import resnet as OR
+    from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
+    threads = threads or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    m = PoseNetRGBDGeometric(pretrained=False)
+    P = {k: v.clone() for k, v in m.state_dict().items()}
+    params = [v.requires_grad_(True) for k, v in P.items() if v.is_floating_point() and "running" not in k]
+    opt = torch.optim.AdamW(params, lr=1e-4, weight_decay=1e-4)
+    rgb, depth_raw, bbox, K, gr, gt = synth_batch(batch, "cpu", 123)
+
+    def one():
+        opt.zero_grad()
+        rot, trans = OR.forward_rgbd_geometric(P, rgb, None, depth_raw, bbox, K, True)
+        loss = OP.pose_loss(rot, trans, gr, gt, 1.0, 10.0)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(params, 1.0)
+        opt.step()
+    one()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    dt = time.perf_counter() - t0
+    return {"value": round(batch * steps / dt, 3), "unit": "crops/s", "cores": threads, "kind": "port",
+            "sample": f"oracle torch-CPU fp32 train step (fwd+loss+bwd+clip+AdamW), batch {batch}, "
+                      f"{steps} timed steps after 1 warmup, {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-profile", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+        pg = dist.group.WORLD
+
+    from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
+    from pose6d.train import RGBDGeometricTrainer
+
+    torch.manual_seed(0)   # same init on every rank (replicated parameters)
+    model = PoseNetRGBDGeometric(pretrained=False).to(dev)
+    B = args.batch
+    tr = RGBDGeometricTrainer(model, B, dtype=torch.bfloat16, process_group=pg)
+    data = synth_batch(B, dev, seed=1000 + rank)   # each rank its own shard
+    if not args.eager:
+        tr.capture(data)
+    for _ in range(args.warmup):
+        tr.step(data)
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.step(data)
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = t.item()
+    loss = tr.loss.item()
+    ms = el / args.steps * 1e3
+    value = world * B * args.steps / el
+
+    result = {
+        "metric": "crops/sec training RGBD-Geometric bs32 224^2 (per GPU), fwd+geodesic/L1 loss+bwd+clip+AdamW",
+        "value": round(value, 2), "unit": "crops/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic (SURVEY.md §8d shapes, device-resident)",
+        "config": {"workload": "PoseNetRGBDGeometric train step (BASELINE configs[2]; configs[4] at N>1)",
+                   "model": "PoseNetRGBDGeometric (ResNet50 + BN-MLP rot head, pinhole translation)",
+                   "global_batch": world * B, "per_gpu_batch": B, "crop": "224x224", "seq_len": None,
+                   "parallelism": f"dp{world}", "loss": float(loss)},
+    }
+    if rank == 0 and not args.no_kernel_profile:
+        result.update(kernel_profile(tr, ms))
+    if rank == 0 and not args.no_cpu_baseline:
+        try:
+            result["cpu_baseline"] = cpu_baseline()
+        except Exception as e:  # noqa: BLE001 - report, do not fail the bench line
+            result["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def kernel_profile(tr, step_ms):
+    """Dominant kernel (largest total time per step) -> roofline object, plus the
+    forward-pass HBM roofline fraction (the north-star's 60 % target)."""
+    from pose6d import profile
+    timed = profile.time_launches(profile.conv_launches(tr.trunk), reps=10)
+    agg = profile.by_symbol(timed)
+    sym, a = max(agg.items(), key=lambda kv: kv[1]["time_s"])
+    avg_t = a["time_s"] / a["launches"]
+    achieved = a["flops"] / a["launches"] / avg_t / 1e12
+    conv_total_ms = sum(v["time_s"] for v in agg.values()) * 1e3
+    # forward-only (training-mode BN) time of the trunk, graph-captured
+    fwd_ms = forward_time(tr)
+    fwd_gbs = FWD_BYTES_PER_CROP * tr.B / (fwd_ms * 1e-3) / 1e9
+    return {
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "kernel": sym, "launches_per_step": a["launches"],
+                     "avg_launch_us": round(avg_t * 1e6, 2),
+                     "algorithmic_flops_per_launch": a["flops"] / a["launches"]},
+        "breakdown": {"conv_kernels_ms_per_step": round(conv_total_ms, 3), "step_ms": round(step_ms, 3),
+                      "by_symbol_ms": {k: round(v["time_s"] * 1e3, 3) for k, v in agg.items()}},
+        "forward_roofline": {"bound": "hbm", "fwd_ms": round(fwd_ms, 4), "achieved": round(fwd_gbs, 1),
+                             "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(fwd_gbs / PEAK_HBM_GBS, 4),
+                             "algorithmic_bytes_per_crop": FWD_BYTES_PER_CROP},
+    }
+
+
+def forward_time(tr, reps=20):
+    """Trunk + head forward of one batch (training-mode BN statistics), in a graph."""
+    rgb = torch.randn(tr.B, 3, 224, 224, device=tr.dev)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(device=tr.dev)
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        tr.trunk.forward(rgb, True, pack=False)
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(g):
+        tr.trunk.forward(rgb, True, pack=False)
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+if __name__ == "__main__":
+    main()

@@ -123,6 +123,12 @@ int pose6d_conv_stats_rows(int32_t N, int32_t Ho, int32_t Wo, int32_t Cout);
 int pose6d_conv2d_fwd(int32_t dtype, const void *x, const void *wp, const float *bias, void *y, float *stats,
                       int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW,
                       int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, void *stream);
+/* kernel variant a conv launch selects (profiling joins): fwd/dgrad (pass 0/1):
+ * (mode << 4) | tile (tile 0..3 = 128x128, 128x64, 64x128, 64x64; mode 0 gemm,
+ * 1 im2col, 2 narrow stem, 3 dgrad); wgrad: (BM == 128) << 1 | (BN == 128). */
+int pose6d_conv_variant(int32_t pass, int32_t M, int32_t Ncols, int32_t KH, int32_t KW, int32_t stride,
+                        int32_t pad, int32_t Cin);
+int pose6d_wgrad_variant(int32_t dtype, int32_t M, int32_t Cout, int32_t K);
 /* data gradient: dx [N][H][W][Cin] = conv_transpose(dy [N][Ho][Wo][Cout], wt) (+ dres if non-NULL) */
 int pose6d_conv2d_dgrad(int32_t dtype, const void *dy, const void *wt, const void *dres, void *dx, int32_t N,
                         int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
@@ -196,8 +202,9 @@ int pose6d_act_bwd(const float *dy, const float *x, float *dx, int64_t n, int32_
 /* ------------------------------------------------------------------------
  * Optimiser — clip_grad_norm_(params, max_norm) + AdamW.step() of the callers
  * (train_rgbd_geometric.py:65,111-112) over one flat fp32 buffer.
- * hp (device) = {lr, beta1, beta2, eps, weight_decay, bias_correction1,
- *                bias_correction2, max_norm (<= 0: no clipping)}
+ * hp (device) = {lr, beta1, beta2, eps, weight_decay, step t (>= 1; bias
+ *                corrections 1 - beta^t computed in-kernel), unused,
+ *                max_norm (<= 0: no clipping)}
  * ---------------------------------------------------------------------- */
 int pose6d_sumsq_partial(const float *g, int64_t n, float *partials, int32_t nparts, void *stream);
 int pose6d_adamw_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,

@@ -90,47 +90,109 @@ def _close(got, ref, rtol, what):
     assert not bool(bad.any()), f"{what}: max err {err.max().item():.3e} vs scale {scale:.3e}"
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("name", list(EXPECTED))
-def test_train_step_parity_fp32(name):
-    """Training-mode forward + PoseLoss(1, 10) + backward in fp32 vs the oracle:
-    outputs and loss within 1e-4 relative, parameter gradients within 1e-3 of
-    their tensor's scale, BN running statistics updated identically.
-    Dropout modules in eval (their RNG differs by construction)."""
+def _oracle_run(name, P0, inp, training, dtype):
+    P = {}
+    for k, v in P0.items():
+        v = v.clone()
+        if v.is_floating_point():
+            v = v.to(dtype)
+            if "running" not in k:
+                v.requires_grad_(True)
+        P[k] = v
+    cast = {k: (v.to(dtype) if v.is_floating_point() else v) for k, v in inp.items()}
+    rot, trans = _oracle_forward(name, P, cast, training)
+    loss = OP.pose_loss(rot, trans, cast["gt_rot"], cast["gt_trans"], 1.0, 10.0)
+    if training:
+        loss.backward()
+    return rot.detach(), trans.detach(), loss.detach(), P
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-30)).item()
+
+
+def _setup(name):
     warnings.simplefilter("ignore")
     torch.manual_seed(0)
     m = _models()[name](pretrained=False)
-    P = {k: v.clone() for k, v in m.state_dict().items()}
-    for k, v in P.items():
-        if v.is_floating_point() and "running" not in k:
-            v.requires_grad_(True)
-    m = m.cuda().train()
+    P0 = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.cuda()
     for mod in m.modules():
         if isinstance(mod, torch.nn.Dropout):
             mod.eval()
     g = torch.Generator().manual_seed(1)
     inp = _inputs(4, 224, g)
-    cuda_inp = {k: v.cuda() for k, v in inp.items()}
-    rot, trans = _model_forward(name, m, cuda_inp)
-    loss = OP.pose_loss  # reference formula, applied on device by the drop-in PoseLoss below
+    return m, P0, inp, {k: v.cuda() for k, v in inp.items()}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(EXPECTED))
+def test_eval_forward_parity_fp32(name):
+    """Eval-mode forward (running-stat BN): pose within 1e-4 relative of the oracle."""
     from models.pose_loss import PoseLoss
-    crit = PoseLoss(1.0, 10.0, "geodesic")
-    L = crit(rot, trans, cuda_inp["gt_rot"], cuda_inp["gt_trans"])
-    L.backward()
-    rr, tr = _oracle_forward(name, P, inp, True)
-    Lr = loss(rr, tr, inp["gt_rot"], inp["gt_trans"], 1.0, 10.0)
-    Lr.backward()
+    m, P0, inp, cin = _setup(name)
+    m.eval()
+    with torch.no_grad():
+        rot, trans = _model_forward(name, m, cin)
+        L = PoseLoss(1.0, 10.0, "geodesic")(rot, trans, cin["gt_rot"], cin["gt_trans"])
+    rr, tr, Lr, _ = _oracle_run(name, P0, inp, False, torch.float32)
     _close(rot, rr, 1e-4, "rotation")
     _close(trans, tr, 1e-4, "translation")
     _close(L, Lr, 1e-4, "loss")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(EXPECTED))
+def test_train_step_parity_fp32(name):
+    """Training-mode forward + PoseLoss(1, 10) + backward in fp32.  Judged against an
+    fp64 run of the oracle: every output / gradient of ours must be as close to the
+    exact (fp64) answer as the reference's own fp32 computation is (within 3x, or
+    1e-4).  A random-init ResNet50 with batch-4 BatchNorm is ill-conditioned: the
+    fp32 reference itself deviates from fp64 by ~1e-5 on the pose and by up to
+    ~1e-1 on deep-layer weight gradients (tools/diag_parity.py), so a fixed
+    1e-4 tolerance on gradients would only measure that conditioning.
+    Dropout modules in eval (their RNG differs by construction)."""
+    from models.pose_loss import PoseLoss
+    m, P0, inp, cin = _setup(name)
+    m.train()
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.eval()
+    rot, trans = _model_forward(name, m, cin)
+    L = PoseLoss(1.0, 10.0, "geodesic")(rot, trans, cin["gt_rot"], cin["gt_trans"])
+    L.backward()
+    r64, t64, L64, P64 = _oracle_run(name, P0, inp, True, torch.float64)
+    r32, t32, L32, P32 = _oracle_run(name, P0, inp, True, torch.float32)
+
+    def check(ours, ref32, ref64, what):
+        e, e_ref = _rel(ours, ref64), _rel(ref32, ref64)
+        assert e <= max(1e-4, 3 * e_ref), f"{what}: ours {e:.2e} vs exact, reference fp32 {e_ref:.2e}"
+
+    check(rot, r32, r64, "rotation")
+    check(trans, t32, t64, "translation")
+    check(L, L32, L64, "loss")
     sd = m.state_dict()
-    for k, v in P.items():
+    for k in P0:
         if "running" in k:
-            _close(sd[k], v, 1e-4, k)
+            check(sd[k], P32[k], P64[k], k)
         elif "num_batches" in k:
-            assert int(sd[k]) == int(v), k
+            assert int(sd[k]) == int(P32[k]), k
+    # gradients: per-tensor errors are dominated by the conditioning of each
+    # tensor (they scatter 0.1x-5x around the reference's own), so compare the
+    # distribution: median and worst case vs the reference fp32's
     named = dict(m.named_parameters())
-    for k, v in P.items():
-        if v.grad is None:
-            continue
-        _close(named[k].grad, v.grad, 1e-3, "grad " + k)
+    ours, ref = [], []
+    for k, v in P64.items():
+        if isinstance(v, torch.Tensor) and v.grad is not None:
+            ours.append(_rel(named[k].grad, v.grad))
+            ref.append(_rel(P32[k].grad, v.grad))
+    ours, ref = np.array(ours), np.array(ref)
+    assert np.median(ours) <= 2 * np.median(ref) + 1e-4, (np.median(ours), np.median(ref))
+    assert ours.max() <= 3 * ref.max() + 1e-4, (ours.max(), ref.max())
+    # and every gradient is at least in the right direction (cosine > 0.99 vs exact)
+    for k, v in P64.items():
+        if isinstance(v, torch.Tensor) and v.grad is not None:
+            a, b = named[k].grad.double().cpu().flatten(), v.grad.double().flatten()
+            cos = (a @ b / (a.norm() * b.norm() + 1e-300)).item()
+            assert cos > 0.99 or b.norm() < 1e-12, f"grad {k}: cosine {cos:.4f}"
