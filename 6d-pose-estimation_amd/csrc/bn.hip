@@ -40,29 +40,61 @@ __device__ __forceinline__ void store_vec(T* p, const float* f) {
 }
 
 // ---------------------------------------------------------------- finalize
+// Chan et al. parallel variance: merge (n, mean, M2) with (nb, mean_b, M2_b)
+struct Welford {
+  double n, mean, m2;
+};
+__device__ __forceinline__ void merge(Welford& a, double nb, double mb, double qb) {
+  if (nb <= 0.0) return;
+  const double n = a.n + nb, d = mb - a.mean;
+  a.mean += d * nb / n;
+  a.m2 += qb + d * d * a.n * nb / n;
+  a.n = n;
+}
+
+constexpr int kSplits = 64;   // stage-1 row chunks
+
+// stage 1: grid (ceil(C/64), splits); rows are the conv epilogue's 32-pixel partials
+// (sum, M2); each block merges its chunk of rows -> ws[split][3][C] = (n, mean, M2)
+__global__ __launch_bounds__(kThreads) void bn_stats_stage1_kernel(const float* __restrict__ part, int rows, int C,
+                                                                   int64_t M, double* __restrict__ ws) {
+  __shared__ double red[3][4][64];
+  const int cl = threadIdx.x & 63, pr = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int s = blockIdx.y, S = gridDim.y;
+  const int r0 = (int)((int64_t)rows * s / S), r1 = (int)((int64_t)rows * (s + 1) / S);
+  Welford w{0.0, 0.0, 0.0};
+  if (c < C)
+    for (int r = r0 + pr; r < r1; r += 4) {
+      const double nb = (double)min((int64_t)32, M - (int64_t)r * 32);
+      merge(w, nb, (double)part[(int64_t)r * 2 * C + c] / nb, (double)part[(int64_t)r * 2 * C + C + c]);
+    }
+  red[0][pr][cl] = w.n;
+  red[1][pr][cl] = w.mean;
+  red[2][pr][cl] = w.m2;
+  __syncthreads();
+  if (pr == 0 && c < C) {
+    for (int k = 1; k < 4; ++k) merge(w, red[0][k][cl], red[1][k][cl], red[2][k][cl]);
+    ws[((int64_t)s * 3 + 0) * C + c] = w.n;
+    ws[((int64_t)s * 3 + 1) * C + c] = w.mean;
+    ws[((int64_t)s * 3 + 2) * C + c] = w.m2;
+  }
+}
+
+// stage 2 (training): merge the splits in order -> batch mean / biased var
 __global__ __launch_bounds__(kThreads) void bn_finalize_kernel(
-    const float* __restrict__ part, int rows, int C, double count, const float* __restrict__ gamma,
+    const double* __restrict__ ws, int splits, int C, double count, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
     float momentum, float eps, int training, float* __restrict__ scale, float* __restrict__ shift,
     float* __restrict__ smean, float* __restrict__ sinv) {
-  __shared__ double red[2][4][64];
-  const int cl = threadIdx.x & 63, pr = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  const int c = blockIdx.x * kThreads + threadIdx.x;
   if (training) {
-    double s = 0.0, q = 0.0;
-    if (c < C)
-      for (int r = pr; r < rows; r += 4) {
-        s += (double)part[(int64_t)r * 2 * C + c];
-        q += (double)part[(int64_t)r * 2 * C + C + c];
-      }
-    red[0][pr][cl] = s;
-    red[1][pr][cl] = q;
-    __syncthreads();
-    if (pr == 0 && c < C) {
-      s = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
-      q = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
-      const double mean = s / count;
-      double var = q / count - mean * mean;
+    if (c < C) {
+      Welford w{0.0, 0.0, 0.0};
+      for (int s = 0; s < splits; ++s)
+        merge(w, ws[((int64_t)s * 3 + 0) * C + c], ws[((int64_t)s * 3 + 1) * C + c], ws[((int64_t)s * 3 + 2) * C + c]);
+      const double mean = w.mean;
+      double var = w.m2 / count;
       if (var < 0.0) var = 0.0;
       const float inv = (float)(1.0 / sqrt(var + (double)eps));
       const float sc = gamma[c] * inv;
@@ -75,7 +107,7 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_kernel(
       rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) nbt[0] += 1;
-  } else if (pr == 0 && c < C) {
+  } else if (c < C) {
     const float inv = 1.0f / sqrtf(rvar[c] + eps);
     const float sc = gamma[c] * inv;
     scale[c] = sc;
@@ -282,10 +314,17 @@ int rows_per_block(int64_t M) {
 extern "C" int pose6d_bn_finalize(const float* partial, int32_t rows, int32_t C, int64_t count, const float* gamma,
                                   const float* beta, float* running_mean, float* running_var, int64_t* num_batches,
                                   float momentum, float eps, int32_t training, float* scale, float* shift,
-                                  float* save_mean, float* save_invstd, void* stream) {
-  P6_CHECK_ARG(C > 0 && (!training || (rows > 0 && count > 0)), "pose6d_bn_finalize: bad sizes");
-  bn_finalize_kernel<<<p6::ceil_div(C, 64), kThreads, 0, p6::stream_of(stream)>>>(
-      partial, rows, C, (double)count, gamma, beta, running_mean, running_var, num_batches, momentum, eps, training,
+                                  float* save_mean, float* save_invstd, double* workspace, void* stream) {
+  P6_CHECK_ARG(C > 0 && (!training || (rows > 0 && count > 0 && workspace)), "pose6d_bn_finalize: bad sizes");
+  hipStream_t s = p6::stream_of(stream);
+  int splits = 0;
+  if (training) {
+    splits = rows < kSplits ? rows : kSplits;
+    bn_stats_stage1_kernel<<<dim3(p6::ceil_div(C, 64), splits), kThreads, 0, s>>>(partial, rows, C, count, workspace);
+    P6_LAUNCH_CHECK();
+  }
+  bn_finalize_kernel<<<p6::ceil_div(C, kThreads), kThreads, 0, s>>>(
+      workspace, splits, C, (double)count, gamma, beta, running_mean, running_var, num_batches, momentum, eps, training,
       scale, shift, save_mean, save_invstd);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;

@@ -233,26 +233,44 @@ __global__ __launch_bounds__(kThreads) void conv_igemm_kernel(const T* __restric
     }
   }
   if (stats) {
-    // per-wave partial sums over this wave's rows; workspace row = (tm * 2 + wm)
+    // partials over blocks of 32 rows (two 16-row MFMA tiles), stats row = m / 32:
+    // (sum, M2 about the block-local mean) -- Chan-mergeable, free of the
+    // E[x^2]-E[x]^2 cancellation; row counts follow from M (pose6d_bn_finalize).
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      float s = 0.f, q = 0.f;
+    for (int h = 0; h < TM / 2; ++h) {
+      const int rb = row_base + h * 32;
+      const int nval = min(max(g.M - rb, 0), 32);
+      const float inv_n = nval > 0 ? 1.0f / (float)nval : 0.f;
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int j = 0; j < TN; ++j) {
+        float s = 0.f;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = row_base + i * 16 + fc * 4 + r;
-          const float v = m < g.M ? acc[i][j][r] : 0.f;
-          s += v;
-          q = fmaf(v, v, q);
+        for (int i = 2 * h; i < 2 * h + 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = row_base + i * 16 + fc * 4 + r;
+            s += m < g.M ? acc[i][j][r] : 0.f;
+          }
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        const float mu = s * inv_n;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 2 * h; i < 2 * h + 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = row_base + i * 16 + fc * 4 + r;
+            const float d = acc[i][j][r] - mu;
+            q = m < g.M ? fmaf(d, d, q) : q;
+          }
+        q += __shfl_xor(q, 16, 64);
+        q += __shfl_xor(q, 32, 64);
+        const int c = col_base + j * 16 + fr;
+        if (lane < 16 && c < g.Ncols && nval > 0) {
+          float* sp = stats + (int64_t)(rb >> 5) * 2 * g.Ncols;
+          sp[c] = s;
+          sp[g.Ncols + c] = q;
         }
-      s += __shfl_xor(s, 16, 64); q += __shfl_xor(q, 16, 64);
-      s += __shfl_xor(s, 32, 64); q += __shfl_xor(q, 32, 64);
-      const int c = col_base + j * 16 + fr;
-      if (lane < 16 && c < g.Ncols) {
-        float* sp = stats + (int64_t)(tm * 2 + wm) * 2 * g.Ncols;
-        sp[c] = s;
-        sp[g.Ncols + c] = q;
       }
     }
   }
@@ -344,11 +362,10 @@ int dispatch(int mode, const Geom& g, int tile, const void* src, const void* w, 
 
 }  // namespace
 
+// statistics rows: one per 32 output pixels (the last may cover fewer)
 extern "C" int pose6d_conv_stats_rows(int32_t N, int32_t Ho, int32_t Wo, int32_t Cout) {
-  const int M = N * Ho * Wo;
-  const int tile = pick_tile(M, Cout);
-  const int bm = (tile == 0 || tile == 1) ? 128 : 64;
-  return 2 * p6::ceil_div(M, bm);
+  (void)Cout;
+  return p6::ceil_div((int64_t)N * Ho * Wo, 32);
 }
 
 extern "C" int pose6d_conv2d_fwd(int32_t dtype, const void* x, const void* w, const float* bias, void* y,

@@ -224,19 +224,40 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const T* __restric
 }
 
 // sum the split slabs (fixed order) into the OIHW fp32 gradient; k = (kh, kw, ci)
-__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw, int Cout, int Kpad, int SC,
-                                    int Cin, int KH, int KW, int splits, int accumulate) {
-  const int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+// block = 32 consecutive (co, k) elements x 8 split-groups: each thread sums every
+// 8th slab (4 independent loads in flight), LDS combines the 8 groups in order.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw,
+                                                           int Cout, int Kpad, int SC, int Cin, int KH, int KW,
+                                                           int splits, int accumulate) {
+  __shared__ float red[8][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int K = KH * KW * SC;
-  if (idx >= (int64_t)Cout * K) return;
-  const int co = idx / K, k = idx - (int64_t)co * K;
-  const int tap = k / SC, ci = k - tap * SC;
-  if (ci >= Cin) return;
-  float s = 0.f;
-  for (int i = 0; i < splits; ++i) s += ws[((int64_t)i * Cout + co) * Kpad + k];
-  const int kh = tap / KW, kw = tap - kh * KW;
-  float* d = dw + (((int64_t)co * Cin + ci) * KH + kh) * KW + kw;
-  *d = accumulate ? *d + s : s;
+  const int64_t idx = blockIdx.x * 32ll + tx;
+  const bool ok = idx < (int64_t)Cout * K;
+  const int co = ok ? (int)(idx / K) : 0, k = ok ? (int)(idx - (int64_t)co * K) : 0;
+  const int64_t slab = (int64_t)Cout * Kpad;
+  const float* p = ws + (int64_t)co * Kpad + k;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int i = ty;
+  if (ok) {
+    for (; i + 24 < splits; i += 32) {
+      a0 += p[i * slab]; a1 += p[(i + 8) * slab]; a2 += p[(i + 16) * slab]; a3 += p[(i + 24) * slab];
+    }
+    for (; i < splits; i += 8) a0 += p[i * slab];
+  }
+  red[ty][tx] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (ty == 0 && ok) {
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) s += red[g][tx];
+    const int tap = k / SC, ci = k - tap * SC;
+    if (ci < Cin) {
+      const int kh = tap / KW, kw = tap - kh * KW;
+      float* d = dw + (((int64_t)co * Cin + ci) * KH + kh) * KW + kw;
+      *d = accumulate ? *d + s : s;
+    }
+  }
 }
 
 struct Plan {
@@ -248,10 +269,13 @@ Plan plan(int M, int Cout, int Kpad) {
   p.bm = Cout >= 128 ? 128 : 64;
   p.bn = Kpad >= 128 ? 128 : 64;
   const int tiles = p6::ceil_div(Cout, p.bm) * p6::ceil_div(Kpad, p.bn);
-  // aim for ~1024 workgroups, each reducing >= 256 pixels
+  // aim for ~1024 workgroups, each reducing >= 256 pixels, slabs <= 16 MB in total
   int splits = p6::ceil_div(1024, tiles);
   const int max_splits = p6::ceil_div(M, 256);
   if (splits > max_splits) splits = max_splits;
+  const int64_t slab = (int64_t)Cout * Kpad * 4;
+  const int max_by_bytes = (int)((16ll << 20) / slab);
+  if (splits > max_by_bytes) splits = max_by_bytes;
   if (splits < 1) splits = 1;
   int mps = p6::ceil_div(p6::ceil_div(M, splits), MT) * MT;
   splits = p6::ceil_div(M, mps);
@@ -314,8 +338,8 @@ extern "C" int pose6d_conv2d_wgrad(int32_t dtype, const void* x, const void* dy,
                                    : launch_any<float>(g, p.bm, p.bn, x, dy, workspace, s);
   if (rc) return rc;
   const int64_t total = (int64_t)Cout * g.K;
-  wgrad_reduce_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(workspace, dw, Cout, g.Kpad, Cin, Cin_real, KH,
-                                                                      KW, g.splits, accumulate);
+  wgrad_reduce_kernel<<<(unsigned)((total + 31) / 32), 256, 0, s>>>(workspace, dw, Cout, g.Kpad, Cin, Cin_real, KH,
+                                                                    KW, g.splits, accumulate);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }

@@ -17,26 +17,29 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(const float* __restr
                                                             const float* __restrict__ B, int64_t sbk, int64_t sbn,
                                                             float* __restrict__ C, int64_t ldc,
                                                             const float* __restrict__ bias, int M, int N, int K,
-                                                            float alpha, float beta) {
+                                                            float alpha, float beta, int kchunk,
+                                                            float* __restrict__ part) {
   __shared__ float As[TBK][TBM + 1];
   __shared__ float Bs[TBK][TBN + 1];
   const int m0 = blockIdx.y * TBM, n0 = blockIdx.x * TBN;
   const int tid = threadIdx.x;
   const int tn = tid % 16, tm = tid / 16;  // each thread: rows tm*2..+1, cols tn*4..+3
   float acc[2][4] = {};
-  for (int k0 = 0; k0 < K; k0 += TBK) {
+  // split-K: this block's K range (part != null -> raw partial sums to part[z])
+  const int kbeg = blockIdx.z * kchunk, kend = min(K, kbeg + kchunk);
+  for (int k0 = kbeg; k0 < kend; k0 += TBK) {
     for (int i = tid; i < TBK * TBM; i += kThreads) {
       // k fastest when A is k-contiguous, m fastest otherwise (coalescing)
       int kk, mm;
       if (sak == 1) { kk = i % TBK; mm = i / TBK; } else { mm = i % TBM; kk = i / TBM; }
       const int m = m0 + mm, k = k0 + kk;
-      As[kk][mm] = (m < M && k < K) ? A[m * sam + k * sak] : 0.f;
+      As[kk][mm] = (m < M && k < kend) ? A[m * sam + k * sak] : 0.f;
     }
     for (int i = tid; i < TBK * TBN; i += kThreads) {
       int kk, nn;
       if (sbk == 1) { kk = i % TBK; nn = i / TBK; } else { nn = i % TBN; kk = i / TBN; }
       const int n = n0 + nn, k = k0 + kk;
-      Bs[kk][nn] = (n < N && k < K) ? B[k * sbk + n * sbn] : 0.f;
+      Bs[kk][nn] = (n < N && k < kend) ? B[k * sbk + n * sbn] : 0.f;
     }
     __syncthreads();
 #pragma unroll 8
@@ -57,12 +60,31 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(const float* __restr
     for (int j = 0; j < 4; ++j) {
       const int m = m0 + tm * 2 + i, n = n0 + tn * 4 + j;
       if (m < M && n < N) {
+        if (part) {
+          part[((int64_t)blockIdx.z * M + m) * N + n] = acc[i][j];
+          continue;
+        }
         float v = alpha * acc[i][j];
         if (bias) v += bias[n];
         if (beta != 0.f) v += beta * C[m * ldc + n];
         C[m * ldc + n] = v;
       }
     }
+}
+
+// C[m][n] = alpha * sum_z part[z][m][n] (+ bias[n]) + beta * C[m][n]   (fixed order)
+__global__ void gemm_splitk_reduce_kernel(const float* __restrict__ part, int splits, float* __restrict__ C,
+                                          int64_t ldc, const float* __restrict__ bias, int M, int N, float alpha,
+                                          float beta) {
+  const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;
+  if (i >= (int64_t)M * N) return;
+  const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
+  float s = 0.f;
+  for (int z = 0; z < splits; ++z) s += part[(int64_t)z * M * N + i];
+  float v = alpha * s;
+  if (bias) v += bias[n];
+  if (beta != 0.f) v += beta * C[m * ldc + n];
+  C[m * ldc + n] = v;
 }
 
 // db[n] (+)= sum_m dy[m][n]
@@ -191,13 +213,32 @@ __global__ void act_bwd_kernel(const float* __restrict__ dy, const float* __rest
 
 extern "C" int pose6d_gemm_f32(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
                                float* C, int64_t ldc, const float* bias, int32_t M, int32_t N, int32_t K, float alpha,
-                               float beta, void* stream) {
+                               float beta, float* workspace, int64_t ws_floats, void* stream) {
   P6_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "pose6d_gemm_f32: bad sizes");
   if (M == 0 || N == 0) return POSE6D_OK;
-  dim3 grid(p6::ceil_div(N, TBN), p6::ceil_div(M, TBM));
-  gemm_f32_kernel<<<grid, kThreads, 0, p6::stream_of(stream)>>>(A, sam, sak, B, sbk, sbn, C, ldc, bias, M, N, K, alpha,
-                                                                beta);
+  hipStream_t s = p6::stream_of(stream);
+  const int tiles = p6::ceil_div(N, TBN) * p6::ceil_div(M, TBM);
+  // skinny (batch-32) GEMMs: split K so that >= ~256 workgroups stream the weights
+  int splits = 1;
+  if (workspace && tiles < 256) {
+    splits = p6::ceil_div(256, tiles);
+    const int by_k = p6::ceil_div(K, 4 * TBK);
+    if (splits > by_k) splits = by_k;
+    const int64_t by_ws = ws_floats / ((int64_t)M * N);
+    if (splits > by_ws) splits = (int)by_ws;
+    if (splits < 1) splits = 1;
+  }
+  const int kchunk = splits > 1 ? p6::ceil_div(p6::ceil_div(K, splits), TBK) * TBK : K;
+  splits = splits > 1 ? p6::ceil_div(K, kchunk) : 1;
+  dim3 grid(p6::ceil_div(N, TBN), p6::ceil_div(M, TBM), splits);
+  gemm_f32_kernel<<<grid, kThreads, 0, s>>>(A, sam, sak, B, sbk, sbn, C, ldc, bias, M, N, K, alpha, beta, kchunk,
+                                            splits > 1 ? workspace : nullptr);
   P6_LAUNCH_CHECK();
+  if (splits > 1) {
+    gemm_splitk_reduce_kernel<<<(unsigned)(((int64_t)M * N + kThreads - 1) / kThreads), kThreads, 0, s>>>(
+        workspace, splits, C, ldc, bias, M, N, alpha, beta);
+    P6_LAUNCH_CHECK();
+  }
   return POSE6D_OK;
 }
 

@@ -2,15 +2,38 @@
 //   pose6d_nchw_to_nhwc      model input (B,C,H,W) fp32 -> NHWC dtype, channels padded
 //   pose6d_pack_conv_weights OIHW fp32 masters -> packed [Cout][Kpad] (+ transposed
 //                            [Cin][KH][KW][Cout] for dgrad), all convs in ONE launch
+//                            (grid.y = conv, grid.z = which layout; writes coalesced)
 //   pose6d_maxpool_fwd/bwd   nn.MaxPool2d (ResNet stem 3x3/s2/p1; z-CNN 2x2/s2);
 //                            first max in window scan order wins (torch CPU), the
-//                            backward gathers in output order (deterministic)
+//                            backward gathers in output order (deterministic);
+//                            one lane per (pixel, 16-byte channel chunk)
 //   pose6d_avgpool_fwd/bwd   nn.AdaptiveAvgPool2d(1) + view(B, -1)
 #include "common.h"
 
 namespace {
 
 constexpr int kThreads = 256;
+
+template <typename T> struct V;
+template <> struct V<bf16> { static constexpr int E = 8; };
+template <> struct V<float> { static constexpr int E = 4; };
+
+template <typename T>
+__device__ __forceinline__ void ld(const T* p, float* f) {
+  constexpr int E = V<T>::E;
+  T t[E];
+  *reinterpret_cast<uint4*>(t) = *reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int e = 0; e < E; ++e) f[e] = p6::to_f(t[e]);
+}
+template <typename T>
+__device__ __forceinline__ void st(T* p, const float* f) {
+  constexpr int E = V<T>::E;
+  T t[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) t[e] = p6::from_f<T>(f[e]);
+  *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(t);
+}
 
 template <typename T>
 __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, T* __restrict__ y, int N, int C, int HW, int Cp) {
@@ -25,100 +48,147 @@ struct PackDesc {
   void* wp;         // [O][Kpad]
   void* wt;         // [I][KH][KW][O] or null
   int O, I, Ip, KH, KW, Kpad;
-  int64_t start, count;  // element range of this conv in the flattened [O][Kpad] index space
+  int64_t start, count;
 };
 
 template <typename T>
-__global__ void pack_kernel(const PackDesc* __restrict__ descs, int nd, int64_t total) {
-  for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < total; i += (int64_t)gridDim.x * kThreads) {
-    int lo = 0, hi = nd - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (descs[mid].start <= i) lo = mid; else hi = mid - 1;
-    }
-    const PackDesc d = descs[lo];
-    const int64_t j = i - d.start;
-    const int o = (int)(j / d.Kpad), k = (int)(j - (int64_t)o * d.Kpad);
+__global__ void pack_kernel(const PackDesc* __restrict__ descs) {
+  const PackDesc d = descs[blockIdx.y];
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  if (blockIdx.z == 0) {          // wp[o][k], k = (kh, kw, ci)
     const int K = d.KH * d.KW * d.Ip;
-    float v = 0.f;
-    int tap = 0, c = 0, kh = 0, kw = 0;
-    if (k < K) {
-      tap = k / d.Ip; c = k - tap * d.Ip; kh = tap / d.KW; kw = tap - kh * d.KW;
-      if (c < d.I) v = d.w[(((int64_t)o * d.I + c) * d.KH + kh) * d.KW + kw];
+    for (int64_t j = blockIdx.x * (int64_t)kThreads + threadIdx.x; j < d.count; j += stride) {
+      const int o = (int)(j / d.Kpad), k = (int)(j - (int64_t)o * d.Kpad);
+      float v = 0.f;
+      if (k < K) {
+        const int tap = k / d.Ip, c = k - tap * d.Ip, kh = tap / d.KW, kw = tap - kh * d.KW;
+        if (c < d.I) v = d.w[(((int64_t)o * d.I + c) * d.KH + kh) * d.KW + kw];
+      }
+      reinterpret_cast<T*>(d.wp)[j] = p6::from_f<T>(v);
     }
-    reinterpret_cast<T*>(d.wp)[j] = p6::from_f<T>(v);
-    if (d.wt && k < K && c < d.I)  // wt[c][kh][kw][o]
-      reinterpret_cast<T*>(d.wt)[(((int64_t)c * d.KH + kh) * d.KW + kw) * d.O + o] = p6::from_f<T>(v);
+  } else if (d.wt) {              // wt[c][kh][kw][o]
+    const int64_t n = (int64_t)d.I * d.KH * d.KW * d.O;
+    for (int64_t j = blockIdx.x * (int64_t)kThreads + threadIdx.x; j < n; j += stride) {
+      const int o = (int)(j % d.O);
+      int64_t r = j / d.O;
+      const int kw = (int)(r % d.KW); r /= d.KW;
+      const int kh = (int)(r % d.KH);
+      const int c = (int)(r / d.KH);
+      reinterpret_cast<T*>(d.wt)[j] = p6::from_f<T>(d.w[(((int64_t)o * d.I + c) * d.KH + kh) * d.KW + kw]);
+    }
   }
 }
 
 template <typename T>
 __global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ idx, int N, int H,
                                    int W, int C, int Ho, int Wo, int k, int s, int p) {
-  const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;  // output element
-  const int64_t total = (int64_t)N * Ho * Wo * C;
-  if (i >= total) return;
-  const int c = i % C;
-  const int64_t pix = i / C;
+  constexpr int E = V<T>::E;
+  const int cpr = C / E;
+  const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;  // (output pixel, chunk)
+  if (i >= (int64_t)N * Ho * Wo * cpr) return;
+  const int c0 = (int)(i % cpr) * E;
+  const int64_t pix = i / cpr;
   const int ox = pix % Wo, oy = (pix / Wo) % Ho, n = pix / ((int64_t)Wo * Ho);
-  float best = -__builtin_inff();
-  int bi = 0;
-  bool any = false;
+  float best[E];
+  uint8_t bi[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) { best[e] = -__builtin_inff(); bi[e] = 0; }
+  bool first = true;
   for (int kh = 0; kh < k; ++kh) {
     const int iy = oy * s - p + kh;
     if (iy < 0 || iy >= H) continue;
     for (int kw = 0; kw < k; ++kw) {
       const int ix = ox * s - p + kw;
       if (ix < 0 || ix >= W) continue;
-      const float v = p6::to_f(x[(((int64_t)n * H + iy) * W + ix) * C + c]);
-      if (!any || v > best || v != v) { best = v; bi = kh * k + kw; any = true; }
+      float v[E];
+      ld(x + (((int64_t)n * H + iy) * W + ix) * C + c0, v);
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if (first || v[e] > best[e] || v[e] != v[e]) { best[e] = v[e]; bi[e] = (uint8_t)(kh * k + kw); }
+      first = false;
     }
   }
-  y[i] = p6::from_f<T>(best);
-  if (idx) idx[i] = (uint8_t)bi;
+  st(y + pix * C + c0, best);
+  if (idx) {
+    if constexpr (E == 8) {
+      uint2 u;
+      __builtin_memcpy(&u, bi, 8);
+      *reinterpret_cast<uint2*>(idx + pix * C + c0) = u;
+    } else {
+      uint32_t u;
+      __builtin_memcpy(&u, bi, 4);
+      *reinterpret_cast<uint32_t*>(idx + pix * C + c0) = u;
+    }
+  }
 }
 
 template <typename T>
 __global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx, T* __restrict__ dx, int N,
                                    int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
-  const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;  // input element
-  const int64_t total = (int64_t)N * H * W * C;
-  if (i >= total) return;
-  const int c = i % C;
-  const int64_t pix = i / C;
+  constexpr int E = V<T>::E;
+  const int cpr = C / E;
+  const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;  // (input pixel, chunk)
+  if (i >= (int64_t)N * H * W * cpr) return;
+  const int c0 = (int)(i % cpr) * E;
+  const int64_t pix = i / cpr;
   const int ix = pix % W, iy = (pix / W) % H, n = pix / ((int64_t)W * H);
   // windows containing (iy, ix): oy*s - p <= iy <= oy*s - p + k - 1
   const int oy0 = max(0, (iy + p - k + s) / s), oy1 = min(Ho - 1, (iy + p) / s);
   const int ox0 = max(0, (ix + p - k + s) / s), ox1 = min(Wo - 1, (ix + p) / s);
-  float g = 0.f;
+  float g[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) g[e] = 0.f;
   for (int oy = oy0; oy <= oy1; ++oy)
     for (int ox = ox0; ox <= ox1; ++ox) {
       const int kh = iy - (oy * s - p), kw = ix - (ox * s - p);
       if (kh < 0 || kw < 0 || kh >= k || kw >= k) continue;
-      const int64_t o = (((int64_t)n * Ho + oy) * Wo + ox) * C + c;
-      if (idx[o] == kh * k + kw) g += p6::to_f(dy[o]);
+      const uint8_t me = (uint8_t)(kh * k + kw);
+      const int64_t o = (((int64_t)n * Ho + oy) * Wo + ox) * C + c0;
+      uint8_t bi[E];
+      __builtin_memcpy(bi, idx + o, E);
+      float d[E];
+      ld(dy + o, d);
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if (bi[e] == me) g[e] += d[e];
     }
-  dx[i] = p6::from_f<T>(g);
+  st(dx + pix * C + c0, g);
 }
 
 template <typename T>
 __global__ void avgpool_fwd_kernel(const T* __restrict__ x, float* __restrict__ y, int N, int HW, int C) {
+  constexpr int E = V<T>::E;
+  const int cpr = C / E;
   const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;
-  if (i >= (int64_t)N * C) return;
-  const int64_t n = i / C;
-  const int c = i % C;
-  float s = 0.f;
-  for (int p = 0; p < HW; ++p) s += p6::to_f(x[(n * HW + p) * C + c]);
-  y[i] = s / (float)HW;
+  if (i >= (int64_t)N * cpr) return;
+  const int64_t n = i / cpr;
+  const int c0 = (int)(i % cpr) * E;
+  float s[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) s[e] = 0.f;
+  for (int p = 0; p < HW; ++p) {
+    float v[E];
+    ld(x + (n * HW + p) * C + c0, v);
+#pragma unroll
+    for (int e = 0; e < E; ++e) s[e] += v[e];
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) y[n * C + c0 + e] = s[e] / (float)HW;
 }
 
 template <typename T>
 __global__ void avgpool_bwd_kernel(const float* __restrict__ dy, T* __restrict__ dx, int N, int HW, int C) {
-  const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;
-  if (i >= (int64_t)N * HW * C) return;
-  const int c = i % C;
-  const int64_t n = i / ((int64_t)HW * C);
-  dx[i] = p6::from_f<T>(dy[n * C + c] / (float)HW);
+  constexpr int E = V<T>::E;
+  const int cpr = C / E;
+  const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;   // (pixel, chunk)
+  if (i >= (int64_t)N * HW * cpr) return;
+  const int c0 = (int)(i % cpr) * E;
+  const int64_t pix = i / cpr;
+  const int64_t n = pix / HW;
+  float v[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) v[e] = dy[n * C + c0 + e] / (float)HW;
+  st(dx + pix * C + c0, v);
 }
 
 inline unsigned blocks(int64_t n) { return (unsigned)((n + kThreads - 1) / kThreads); }
@@ -145,28 +215,35 @@ extern "C" int pose6d_pack_desc_size(void) { return (int)sizeof(PackDesc); }
 
 extern "C" int pose6d_pack_conv_weights(int32_t dtype, const void* descs, int32_t n_desc, int64_t total,
                                         void* stream) {
-  if (total == 0 || n_desc == 0) return POSE6D_OK;
+  (void)total;
+  if (n_desc == 0) return POSE6D_OK;
+  P6_CHECK_ARG(n_desc <= 65535, "pose6d_pack_conv_weights: too many descriptors");
   hipStream_t s = p6::stream_of(stream);
-  unsigned g = blocks(total);
-  if (g > 8192) g = 8192;
-  if (dtype == POSE6D_DT_BF16) pack_kernel<bf16><<<g, kThreads, 0, s>>>((const PackDesc*)descs, n_desc, total);
-  else pack_kernel<float><<<g, kThreads, 0, s>>>((const PackDesc*)descs, n_desc, total);
+  dim3 grid(128, n_desc, 2);
+  if (dtype == POSE6D_DT_BF16) pack_kernel<bf16><<<grid, kThreads, 0, s>>>((const PackDesc*)descs);
+  else pack_kernel<float><<<grid, kThreads, 0, s>>>((const PackDesc*)descs);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
+
+#define P6_POOL_CHECK(C, dtype) \
+  P6_CHECK_ARG((C) % ((dtype) == POSE6D_DT_BF16 ? 8 : 4) == 0, "%s: C %% vector width != 0", __func__)
 
 extern "C" int pose6d_maxpool_fwd(int32_t dtype, const void* x, void* y, uint8_t* argmax, int32_t N, int32_t H,
                                   int32_t W, int32_t C, int32_t k, int32_t s, int32_t p, int32_t Ho, int32_t Wo,
                                   void* stream) {
   P6_CHECK_ARG(k * k <= 255, "pose6d_maxpool_fwd: window too large");
-  const int64_t n = (int64_t)N * Ho * Wo * C;
-  if (n == 0) return POSE6D_OK;
-  hipStream_t st = p6::stream_of(stream);
-  if (dtype == POSE6D_DT_BF16)
-    maxpool_fwd_kernel<bf16><<<blocks(n), kThreads, 0, st>>>((const bf16*)x, (bf16*)y, argmax, N, H, W, C, Ho, Wo, k, s, p);
-  else
-    maxpool_fwd_kernel<float><<<blocks(n), kThreads, 0, st>>>((const float*)x, (float*)y, argmax, N, H, W, C, Ho, Wo, k, s,
-                                                               p);
+  P6_POOL_CHECK(C, dtype);
+  hipStream_t st_ = p6::stream_of(stream);
+  if (dtype == POSE6D_DT_BF16) {
+    const int64_t n = (int64_t)N * Ho * Wo * (C / 8);
+    if (n) maxpool_fwd_kernel<bf16><<<blocks(n), kThreads, 0, st_>>>((const bf16*)x, (bf16*)y, argmax, N, H, W, C, Ho,
+                                                                       Wo, k, s, p);
+  } else {
+    const int64_t n = (int64_t)N * Ho * Wo * (C / 4);
+    if (n) maxpool_fwd_kernel<float><<<blocks(n), kThreads, 0, st_>>>((const float*)x, (float*)y, argmax, N, H, W, C, Ho,
+                                                                        Wo, k, s, p);
+  }
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
@@ -174,37 +251,43 @@ extern "C" int pose6d_maxpool_fwd(int32_t dtype, const void* x, void* y, uint8_t
 extern "C" int pose6d_maxpool_bwd(int32_t dtype, const void* dy, const uint8_t* argmax, void* dx, int32_t N, int32_t H,
                                   int32_t W, int32_t C, int32_t k, int32_t s, int32_t p, int32_t Ho, int32_t Wo,
                                   void* stream) {
-  const int64_t n = (int64_t)N * H * W * C;
-  if (n == 0) return POSE6D_OK;
-  hipStream_t st = p6::stream_of(stream);
-  if (dtype == POSE6D_DT_BF16)
-    maxpool_bwd_kernel<bf16><<<blocks(n), kThreads, 0, st>>>((const bf16*)dy, argmax, (bf16*)dx, N, H, W, C, Ho, Wo, k, s,
-                                                              p);
-  else
-    maxpool_bwd_kernel<float><<<blocks(n), kThreads, 0, st>>>((const float*)dy, argmax, (float*)dx, N, H, W, C, Ho, Wo, k,
-                                                               s, p);
+  P6_POOL_CHECK(C, dtype);
+  hipStream_t st_ = p6::stream_of(stream);
+  if (dtype == POSE6D_DT_BF16) {
+    const int64_t n = (int64_t)N * H * W * (C / 8);
+    if (n) maxpool_bwd_kernel<bf16><<<blocks(n), kThreads, 0, st_>>>((const bf16*)dy, argmax, (bf16*)dx, N, H, W, C, Ho,
+                                                                       Wo, k, s, p);
+  } else {
+    const int64_t n = (int64_t)N * H * W * (C / 4);
+    if (n) maxpool_bwd_kernel<float><<<blocks(n), kThreads, 0, st_>>>((const float*)dy, argmax, (float*)dx, N, H, W, C,
+                                                                        Ho, Wo, k, s, p);
+  }
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
 
 extern "C" int pose6d_avgpool_fwd(int32_t dtype, const void* x, float* y, int32_t N, int32_t HW, int32_t C,
                                   void* stream) {
-  const int64_t n = (int64_t)N * C;
+  P6_POOL_CHECK(C, dtype);
+  hipStream_t st_ = p6::stream_of(stream);
+  const int E = dtype == POSE6D_DT_BF16 ? 8 : 4;
+  const int64_t n = (int64_t)N * (C / E);
   if (n == 0) return POSE6D_OK;
-  hipStream_t st = p6::stream_of(stream);
-  if (dtype == POSE6D_DT_BF16) avgpool_fwd_kernel<bf16><<<blocks(n), kThreads, 0, st>>>((const bf16*)x, y, N, HW, C);
-  else avgpool_fwd_kernel<float><<<blocks(n), kThreads, 0, st>>>((const float*)x, y, N, HW, C);
+  if (dtype == POSE6D_DT_BF16) avgpool_fwd_kernel<bf16><<<blocks(n), kThreads, 0, st_>>>((const bf16*)x, y, N, HW, C);
+  else avgpool_fwd_kernel<float><<<blocks(n), kThreads, 0, st_>>>((const float*)x, y, N, HW, C);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
 
 extern "C" int pose6d_avgpool_bwd(int32_t dtype, const float* dy, void* dx, int32_t N, int32_t HW, int32_t C,
                                   void* stream) {
-  const int64_t n = (int64_t)N * HW * C;
+  P6_POOL_CHECK(C, dtype);
+  hipStream_t st_ = p6::stream_of(stream);
+  const int E = dtype == POSE6D_DT_BF16 ? 8 : 4;
+  const int64_t n = (int64_t)N * HW * (C / E);
   if (n == 0) return POSE6D_OK;
-  hipStream_t st = p6::stream_of(stream);
-  if (dtype == POSE6D_DT_BF16) avgpool_bwd_kernel<bf16><<<blocks(n), kThreads, 0, st>>>(dy, (bf16*)dx, N, HW, C);
-  else avgpool_bwd_kernel<float><<<blocks(n), kThreads, 0, st>>>(dy, (float*)dx, N, HW, C);
+  if (dtype == POSE6D_DT_BF16) avgpool_bwd_kernel<bf16><<<blocks(n), kThreads, 0, st_>>>(dy, (bf16*)dx, N, HW, C);
+  else avgpool_bwd_kernel<float><<<blocks(n), kThreads, 0, st_>>>(dy, (float*)dx, N, HW, C);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }

@@ -84,6 +84,8 @@ class HeadEngine:
                 st.smean = torch.empty(d, device=device, dtype=torch.float32)
                 st.sinv = torch.empty(d, device=device, dtype=torch.float32)
         self.out_dim = d
+        widest = max([in_dim] + [st.dim for st in self.stages])
+        self.ws = torch.empty(16 * B * widest, device=device, dtype=torch.float32)   # split-K partials
 
     def forward(self, x, training, seed_dev=None, salt=0):
         """x: (B, in) fp32 device tensor -> (B, out) (engine buffer)."""
@@ -100,7 +102,8 @@ class HeadEngine:
                 m = st.mod
                 K, N = m.in_features, m.out_features
                 call("gemm_f32", cur, K, 1, m.weight.detach(), 1, K, st.y, N,
-                     m.bias.detach() if m.bias is not None else None, B, N, K, 1.0, 0.0, st_)
+                     m.bias.detach() if m.bias is not None else None, B, N, K, 1.0, 0.0, self.ws, self.ws.numel(),
+                     st_)
             else:
                 # per-module flags, as nn.Dropout / nn.BatchNorm1d themselves behave
                 p = float(st.drop.p) if (st.drop is not None and st.drop.training and st.drop.p > 0) else 0.0
@@ -137,12 +140,14 @@ class HeadEngine:
                 m = st.mod
                 K, N = m.in_features, m.out_features
                 # dW[N][K] = dy^T x
-                call("gemm_f32", g, 1, N, st.x, K, 1, grad_of(m.weight), K, None, N, K, B, 1.0, float(acc), st_)
+                call("gemm_f32", g, 1, N, st.x, K, 1, grad_of(m.weight), K, None, N, K, B, 1.0, float(acc),
+                     self.ws, self.ws.numel(), st_)
                 if m.bias is not None:
                     call("colsum_f32", g, grad_of(m.bias), B, N, acc, st_)
                 if last and not need_dx:
                     return None
-                call("gemm_f32", g, N, 1, m.weight.detach(), K, 1, st.dx, K, None, B, K, N, 1.0, 0.0, st_)
+                call("gemm_f32", g, N, 1, m.weight.detach(), K, 1, st.dx, K, None, B, K, N, 1.0, 0.0, self.ws,
+                     self.ws.numel(), st_)
             elif st.kind == "bn1d":
                 bn = st.mod
                 call("bn1d_bwd", g, st.x, st.y, B, st.dim, bn.weight.detach(), st.smean, st.sinv,

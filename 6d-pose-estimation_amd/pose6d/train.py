@@ -71,6 +71,7 @@ class RGBDGeometricTrainer:
         model.train()
         self.trunk = TrunkEngine(model.backbone, 3)
         self.trunk.set_dtype(dtype)
+        self.trunk.prepare(batch, 224, 224, dtype, dev)
         self.head = HeadEngine(model.rot_head)
         order = self.head.params_in_grad_order() + self.trunk.params_in_grad_order()
         assert len(order) == len(list(model.parameters())) and {id(p) for p in order} == \

@@ -100,6 +100,7 @@ class TrunkEngine:
         self.generation = 0
         self._saved_gen = -1
         self._pack_key = None
+        self._build(224, 224)   # op graph (geometry is re-derived in prepare())
 
     # ------------------------------------------------------------ graph build
     def _build(self, H, W):
@@ -194,6 +195,7 @@ class TrunkEngine:
                 op.argmax = torch.empty(B, o.H, o.W, o.C, device=device, dtype=torch.uint8)
         self.ws_wgrad = f32(max(ws_w // 4, 1))
         self.ws_bn = f32(max(ws_bn, 1))
+        self.ws_fin = torch.empty(64 * 3 * max(op.cout for op in self.convs), device=device, dtype=torch.float64)
         self.feat = f32(B, self.feat_dim)
         self.feat_grad_in = None
         # weight packing descriptors (one launch for all convs)
@@ -254,7 +256,7 @@ class TrunkEngine:
                 call("bn_finalize", op.stats, op.stats_rows, op.cout, B * op.Ho * op.Wo, bn.weight.detach(),
                      bn.bias.detach(), bn.running_mean, bn.running_var, bn.num_batches_tracked,
                      float(bn.momentum if bn.momentum is not None else 0.1), float(bn.eps), int(training),
-                     op.scale, op.shift, op.mean, op.inv, st)
+                     op.scale, op.shift, op.mean, op.inv, self.ws_fin, st)
             elif isinstance(op, _ActOp):
                 c = op.cop
                 M = B * c.Ho * c.Wo

@@ -144,11 +144,14 @@ int pose6d_conv2d_wgrad(int32_t dtype, const void *x, const void *dy, float *dw,
 
 /* nn.BatchNorm2d: finalize the conv-epilogue statistics (training) or use the
  * running statistics (eval) -> scale/shift (+ saved mean / invstd); running
- * stats, num_batches_tracked updated in training (torch semantics). */
+ * stats, num_batches_tracked updated in training (torch semantics).
+ * partial: `rows` = ceil(count / 32) rows of [2][C] (sum, M2 about the row's mean)
+ * over 32-pixel blocks; merged with Chan's parallel-variance formula in fp64
+ * (two launches); workspace: 64 * 3 * C doubles. */
 int pose6d_bn_finalize(const float *partial, int32_t rows, int32_t C, int64_t count, const float *gamma,
                        const float *beta, float *running_mean, float *running_var, int64_t *num_batches,
                        float momentum, float eps, int32_t training, float *scale, float *shift, float *save_mean,
-                       float *save_invstd, void *stream);
+                       float *save_invstd, double *workspace, void *stream);
 /* out = act(y * scale + shift [+ res | + res * res_scale + res_shift]); act = ReLU if relu */
 int pose6d_bn_act_fwd(int32_t dtype, const void *y, const float *scale, const float *shift, const void *res,
                       const float *res_scale, const float *res_shift, int32_t relu, void *out, int64_t M, int32_t C,
@@ -179,10 +182,12 @@ int pose6d_avgpool_bwd(int32_t dtype, const float *dy, void *dx, int32_t N, int3
  * of the rot/trans/z heads (pose_net_rgb.py:23-50, pose_net_rgbd_geometric.py:28-38,
  * pose_net_rgb_geometric.py:23-33,58-65, pose_net_rgbd.py:73-103).
  * ---------------------------------------------------------------------- */
-/* C[m][n] = alpha * sum_k A[m*sam + k*sak] * B[k*sbk + n*sbn] (+ bias[n]) + beta * C[m][n] */
+/* C[m][n] = alpha * sum_k A[m*sam + k*sak] * B[k*sbk + n*sbn] (+ bias[n]) + beta * C[m][n]
+ * workspace (may be NULL): ws_floats fp32 for split-K partials of skinny GEMMs
+ * (reduced in fixed order; >= 16 * M * N floats enables the full split). */
 int pose6d_gemm_f32(const float *A, int64_t sam, int64_t sak, const float *B, int64_t sbk, int64_t sbn, float *C,
                     int64_t ldc, const float *bias, int32_t M, int32_t N, int32_t K, float alpha, float beta,
-                    void *stream);
+                    float *workspace, int64_t ws_floats, void *stream);
 int pose6d_colsum_f32(const float *dy, float *db, int32_t M, int32_t N, int32_t accumulate, void *stream);
 /* BatchNorm1d (+ReLU) (+Dropout p_drop with a counter-based RNG keyed by the
  * device word *seed xor salt -- a device word so graph replays draw new masks) */

@@ -66,9 +66,18 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
     yr = F.conv2d(xr, wr, b, stride=s, padding=p)
     tol = 1e-4 if dtype == torch.float32 else 2e-2
     _close(y.permute(0, 3, 1, 2), yr.detach(), tol, "fwd")
-    st = stats.sum(0).cpu()
-    _close(st[0], yr.detach().sum((0, 2, 3)), 1e-4 if dtype == torch.float32 else 1e-2, "stats.sum")
-    _close(st[1], (yr.detach() ** 2).sum((0, 2, 3)), 1e-4 if dtype == torch.float32 else 1e-2, "stats.sumsq")
+    # epilogue statistics -> finalize: batch mean / biased variance of the fp32 accumulators
+    C = Cout
+    one, zero = torch.ones(C, device=dev), torch.zeros(C, device=dev)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    sc, sh, mu, iv = (torch.empty(C, device=dev) for _ in range(4))
+    ws = torch.empty(64 * 3 * C, device=dev, dtype=torch.float64)
+    call("bn_finalize", stats, rows, C, N * Ho * Wo, one, zero, rm, rv, None, 0.1, 1e-5, 1, sc, sh, mu, iv, ws,
+         stream())
+    ref = yr.detach().double()
+    _close(mu, ref.mean((0, 2, 3)), 1e-4 if dtype == torch.float32 else 1e-2, "batch mean")
+    var = 1.0 / iv.double().cpu() ** 2 - 1e-5
+    _close(var, ref.var((0, 2, 3), unbiased=False), 1e-4 if dtype == torch.float32 else 1e-2, "batch var")
 
     dy = torch.randn(N, Cout, Ho, Wo, generator=g)
     if dtype == torch.bfloat16:
@@ -108,12 +117,21 @@ def test_bn_act_and_backward(dtype):
     gamma = torch.rand(C, generator=g) + 0.5
     beta = torch.randn(C, generator=g)
     dev, dt = "cuda", DTYPES[dtype]
-    # statistics partials as the conv epilogue would emit them (one row)
-    stats = torch.stack([y.sum((0, 2, 3)), (y * y).sum((0, 2, 3))]).reshape(1, 2, C).to(dev)
+    # statistics partials as the conv epilogue emits them: per 32 pixels (sum, M2)
+    flat = y.permute(0, 2, 3, 1).reshape(M, C).double()
+    rows = (M + 31) // 32
+    part = torch.zeros(rows, 2, C, dtype=torch.float64)
+    for r in range(rows):
+        blk = flat[32 * r:32 * r + 32]
+        part[r, 0] = blk.sum(0)
+        part[r, 1] = ((blk - blk.mean(0)) ** 2).sum(0)
+    stats = part.float().to(dev)
     rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
     nbt = torch.zeros((), dtype=torch.long, device=dev)
     sc, sh, mu, iv = (torch.empty(C, device=dev) for _ in range(4))
-    call("bn_finalize", stats, 1, C, M, gamma.to(dev), beta.to(dev), rm, rv, nbt, 0.1, 1e-5, 1, sc, sh, mu, iv, stream())
+    ws = torch.empty(64 * 3 * C, device=dev, dtype=torch.float64)
+    call("bn_finalize", stats, rows, C, M, gamma.to(dev), beta.to(dev), rm, rv, nbt, 0.1, 1e-5, 1, sc, sh, mu, iv, ws,
+         stream())
     yd, rd = _nhwc(y).to(dev, dtype), _nhwc(res).to(dev, dtype)
     out = torch.empty_like(yd)
     call("bn_act_fwd", dt, yd, sc, sh, rd, None, None, 1, out, M, C, stream())

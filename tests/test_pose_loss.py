@@ -14,8 +14,9 @@ RTOL = 1e-4
 def _well_conditioned(pr, gr, kind):
     q1 = pr / np.maximum(np.linalg.norm(pr.astype(np.float64), axis=1, keepdims=True), 1e-12)
     q2 = gr / np.linalg.norm(gr.astype(np.float64), axis=1, keepdims=True)
-    if kind != "geodesic":   # |.| of components that are ~0 up to rounding: sign noise
-        return (np.abs(q1 - q2).min(1) > 1e-5) & (np.abs(q1 + q2).min(1) > 1e-5)
+    if kind != "geodesic":   # |.| of components ~0, or min() of two ~equal sums: rounding decides
+        dp, dm = np.abs(q1 - q2).sum(1), np.abs(q1 + q2).sum(1)
+        return (np.abs(q1 - q2).min(1) > 1e-5) & (np.abs(q1 + q2).min(1) > 1e-5) & (np.abs(dp - dm) > 1e-5)
     dot = (q1 * q2).sum(1, keepdims=True)
     q2 = np.where(dot < 0, -q2, q2)
     # the double-cover flip (pose_loss.py:40) is decided by the sign of a rounded dot
