@@ -54,27 +54,39 @@ __device__ __forceinline__ void merge(Welford& a, double nb, double mb, double q
 
 constexpr int kSplits = 64;   // stage-1 row chunks
 
-// stage 1: grid (ceil(C/64), splits); rows are the conv epilogue's 32-pixel partials
-// (sum, M2); each block merges its chunk of rows -> ws[split][3][C] = (n, mean, M2)
+// stage 1: grid (ceil(C/16), splits); rows are the conv epilogue's 32-pixel partials
+// (sum, M2); block = 16 channels x 16 lanes merges its chunk of rows (lane l takes
+// rows l, l+16, ... two loads in flight), lane 0 merges the lanes in order
+// -> ws[split][3][C] = (n, mean, M2)
 __global__ __launch_bounds__(kThreads) void bn_stats_stage1_kernel(const float* __restrict__ part, int rows, int C,
                                                                    int64_t M, double* __restrict__ ws) {
-  __shared__ double red[3][4][64];
-  const int cl = threadIdx.x & 63, pr = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  __shared__ double red[3][16][17];
+  const int cl = threadIdx.x & 15, ln = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   const int s = blockIdx.y, S = gridDim.y;
   const int r0 = (int)((int64_t)rows * s / S), r1 = (int)((int64_t)rows * (s + 1) / S);
   Welford w{0.0, 0.0, 0.0};
-  if (c < C)
-    for (int r = r0 + pr; r < r1; r += 4) {
+  if (c < C) {
+    int r = r0 + ln;
+    for (; r + 16 < r1; r += 32) {
+      const float s0 = part[(int64_t)r * 2 * C + c], q0 = part[(int64_t)r * 2 * C + C + c];
+      const float s1 = part[(int64_t)(r + 16) * 2 * C + c], q1 = part[(int64_t)(r + 16) * 2 * C + C + c];
+      const double n0 = (double)min((int64_t)32, M - (int64_t)r * 32);
+      const double n1 = (double)min((int64_t)32, M - (int64_t)(r + 16) * 32);
+      merge(w, n0, (double)s0 / n0, (double)q0);
+      merge(w, n1, (double)s1 / n1, (double)q1);
+    }
+    if (r < r1) {
       const double nb = (double)min((int64_t)32, M - (int64_t)r * 32);
       merge(w, nb, (double)part[(int64_t)r * 2 * C + c] / nb, (double)part[(int64_t)r * 2 * C + C + c]);
     }
-  red[0][pr][cl] = w.n;
-  red[1][pr][cl] = w.mean;
-  red[2][pr][cl] = w.m2;
+  }
+  red[0][cl][ln] = w.n;
+  red[1][cl][ln] = w.mean;
+  red[2][cl][ln] = w.m2;
   __syncthreads();
-  if (pr == 0 && c < C) {
-    for (int k = 1; k < 4; ++k) merge(w, red[0][k][cl], red[1][k][cl], red[2][k][cl]);
+  if (ln == 0 && c < C) {
+    for (int k = 1; k < 16; ++k) merge(w, red[0][cl][k], red[1][cl][k], red[2][cl][k]);
     ws[((int64_t)s * 3 + 0) * C + c] = w.n;
     ws[((int64_t)s * 3 + 1) * C + c] = w.mean;
     ws[((int64_t)s * 3 + 2) * C + c] = w.m2;
@@ -87,12 +99,30 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_kernel(
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
     float momentum, float eps, int training, float* __restrict__ scale, float* __restrict__ shift,
     float* __restrict__ smean, float* __restrict__ sinv) {
-  const int c = blockIdx.x * kThreads + threadIdx.x;
+  // block = 16 channels x 16 lanes; lane l merges splits l, l+16, ... (loads issued
+  // together), then lane 0 merges the 16 lane results in order (deterministic)
+  __shared__ double red[3][16][17];
+  const int cl = threadIdx.x & 15, ln = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   if (training) {
+    Welford w{0.0, 0.0, 0.0};
     if (c < C) {
-      Welford w{0.0, 0.0, 0.0};
-      for (int s = 0; s < splits; ++s)
-        merge(w, ws[((int64_t)s * 3 + 0) * C + c], ws[((int64_t)s * 3 + 1) * C + c], ws[((int64_t)s * 3 + 2) * C + c]);
+      double v[kSplits / 16][3];
+#pragma unroll
+      for (int i = 0; i < kSplits / 16; ++i) {
+        const int s = ln + 16 * i;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) v[i][k] = s < splits ? ws[((int64_t)s * 3 + k) * C + c] : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < kSplits / 16; ++i) merge(w, v[i][0], v[i][1], v[i][2]);
+    }
+    red[0][cl][ln] = w.n;
+    red[1][cl][ln] = w.mean;
+    red[2][cl][ln] = w.m2;
+    __syncthreads();
+    if (ln == 0 && c < C) {
+      for (int k = 1; k < 16; ++k) merge(w, red[0][cl][k], red[1][cl][k], red[2][cl][k]);
       const double mean = w.mean;
       double var = w.m2 / count;
       if (var < 0.0) var = 0.0;
@@ -107,7 +137,7 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_kernel(
       rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) nbt[0] += 1;
-  } else if (c < C) {
+  } else if (c < C && ln == 0) {
     const float inv = 1.0f / sqrtf(rvar[c] + eps);
     const float sc = gamma[c] * inv;
     scale[c] = sc;
@@ -222,21 +252,31 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_finalize_kernel(const float* 
                                                                    const float* __restrict__ inv,
                                                                    float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                                    int accumulate, float* __restrict__ coef) {
-  __shared__ double red[2][4][64];
-  const int cl = threadIdx.x & 63, pr = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  // block = 16 channels x 16 lanes (4 independent loads in flight per lane)
+  __shared__ double red[2][16][17];
+  const int cl = threadIdx.x & 15, ln = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   double s = 0.0, q = 0.0;
-  if (c < C)
-    for (int r = pr; r < rows; r += 4) {
+  if (c < C) {
+    int r = ln;
+    for (; r + 48 < rows; r += 64) {
+      const float* p = part + (int64_t)r * 2 * C + c;
+      const int64_t st = (int64_t)16 * 2 * C;
+      const float s0 = p[0], s1 = p[st], s2 = p[2 * st], s3 = p[3 * st];
+      const float q0 = p[C], q1 = p[st + C], q2 = p[2 * st + C], q3 = p[3 * st + C];
+      s += ((double)s0 + s1) + ((double)s2 + s3);
+      q += ((double)q0 + q1) + ((double)q2 + q3);
+    }
+    for (; r < rows; r += 16) {
       s += (double)part[(int64_t)r * 2 * C + c];
       q += (double)part[(int64_t)r * 2 * C + C + c];
     }
-  red[0][pr][cl] = s;
-  red[1][pr][cl] = q;
+  }
+  red[0][cl][ln] = s;
+  red[1][cl][ln] = q;
   __syncthreads();
-  if (pr == 0 && c < C) {
-    s = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
-    q = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+  if (ln == 0 && c < C) {
+    for (int k = 1; k < 16; ++k) { s += red[0][cl][k]; q += red[1][cl][k]; }
     if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)s;
     if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)q;
     coef[c] = gamma[c] * inv[c];            // c1
@@ -320,10 +360,10 @@ extern "C" int pose6d_bn_finalize(const float* partial, int32_t rows, int32_t C,
   int splits = 0;
   if (training) {
     splits = rows < kSplits ? rows : kSplits;
-    bn_stats_stage1_kernel<<<dim3(p6::ceil_div(C, 64), splits), kThreads, 0, s>>>(partial, rows, C, count, workspace);
+    bn_stats_stage1_kernel<<<dim3(p6::ceil_div(C, 16), splits), kThreads, 0, s>>>(partial, rows, C, count, workspace);
     P6_LAUNCH_CHECK();
   }
-  bn_finalize_kernel<<<p6::ceil_div(C, kThreads), kThreads, 0, s>>>(
+  bn_finalize_kernel<<<p6::ceil_div(C, 16), kThreads, 0, s>>>(
       workspace, splits, C, (double)count, gamma, beta, running_mean, running_var, num_batches, momentum, eps, training,
       scale, shift, save_mean, save_invstd);
   P6_LAUNCH_CHECK();
@@ -364,7 +404,7 @@ extern "C" int pose6d_bn_bwd(int32_t dtype, const void* dout, const void* out, c
         (const float*)dout, (const float*)out, (const float*)y, mean, invstd, part, M, C, rpb);
   }
   P6_LAUNCH_CHECK();
-  bn_bwd_finalize_kernel<<<p6::ceil_div(C, 64), kThreads, 0, s>>>(part, nb, C, (double)M, gamma, invstd, dgamma, dbeta,
+  bn_bwd_finalize_kernel<<<p6::ceil_div(C, 16), kThreads, 0, s>>>(part, nb, C, (double)M, gamma, invstd, dgamma, dbeta,
                                                                   accumulate, coef);
   P6_LAUNCH_CHECK();
   if (dtype == POSE6D_DT_BF16)
