@@ -17,6 +17,9 @@
 // the fp32 accumulators -> stats workspace, reduced by pose6d_bn_finalize), the
 // tile goes through LDS so that global stores are whole 16-byte chunks of
 // contiguous NHWC rows, optionally adding a residual tensor (dgrad: dX += dRes).
+#include <stdlib.h>
+#include <string.h>
+
 #include "common.h"
 
 namespace {
@@ -41,6 +44,103 @@ struct Geom {
 // block; this XOR makes every 16-lane LDS group hit 16 distinct 16-byte slots.
 __device__ __forceinline__ int swz(int row) { return (4 - ((row >> 2) & 3)) & 3; }
 
+// Shared epilogue: + bias, BatchNorm partial statistics, LDS-staged 16-B stores
+// (+ residual).  Must be entered after a barrier that ends all LDS reads.
+template <typename T, int BM, int BN>
+__device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const Geom& g,
+                                              const float* __restrict__ bias, const T* __restrict__ res,
+                                              T* __restrict__ out, float* __restrict__ stats, int m0, int n0) {
+  constexpr int TM = BM / 32, TN = BN / 32;
+  constexpr int CROW = BN * (int)sizeof(T) + 16;  // epilogue tile row stride (bytes)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fc = lane >> 4;
+  const int row_base = m0 + wm * (BM / 2);
+  const int col_base = n0 + wn * (BN / 2);
+  if (bias) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int c = col_base + j * 16 + fr;
+      const float bv = c < g.Ncols ? bias[c] : 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[i][j] += bv;
+    }
+  }
+  if (stats) {
+    // partials over blocks of 32 rows (two 16-row MFMA tiles), stats row = m / 32:
+    // (sum, M2 about the block-local mean) -- Chan-mergeable, free of the
+    // E[x^2]-E[x]^2 cancellation; row counts follow from M (pose6d_bn_finalize).
+#pragma unroll
+    for (int h = 0; h < TM / 2; ++h) {
+      const int rb = row_base + h * 32;
+      const int nval = min(max(g.M - rb, 0), 32);
+      const float inv_n = nval > 0 ? 1.0f / (float)nval : 0.f;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 2 * h; i < 2 * h + 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = row_base + i * 16 + fc * 4 + r;
+            s += m < g.M ? acc[i][j][r] : 0.f;
+          }
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        const float mu = s * inv_n;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 2 * h; i < 2 * h + 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = row_base + i * 16 + fc * 4 + r;
+            const float d = acc[i][j][r] - mu;
+            q = m < g.M ? fmaf(d, d, q) : q;
+          }
+        q += __shfl_xor(q, 16, 64);
+        q += __shfl_xor(q, 32, 64);
+        const int c = col_base + j * 16 + fr;
+        if (lane < 16 && c < g.Ncols && nval > 0) {
+          float* sp = stats + (int64_t)(rb >> 5) * 2 * g.Ncols;
+          sp[c] = s;
+          sp[g.Ncols + c] = q;
+        }
+      }
+    }
+  }
+  // stage the tile through LDS (staging buffers are dead after the final barrier)
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lr = wm * (BM / 2) + i * 16 + fc * 4 + r;
+        const int lc = wn * (BN / 2) + j * 16 + fr;
+        *reinterpret_cast<T*>(smem + lr * CROW + lc * (int)sizeof(T)) = p6::from_f<T>(acc[i][j][r]);
+      }
+  __syncthreads();
+  constexpr int CPR = BN * (int)sizeof(T) / 16;  // 16-B chunks per tile row
+  for (int idx = tid; idx < BM * CPR; idx += kThreads) {
+    const int lr = idx / CPR, cc = idx - lr * CPR;
+    const int m = m0 + lr, c = n0 + cc * (16 / (int)sizeof(T));
+    if (m >= g.M || c >= g.Ncols) continue;
+    uint4 v = *reinterpret_cast<const uint4*>(smem + lr * CROW + cc * 16);
+    T* dst = out + (int64_t)m * g.Ncols + c;
+    if (res) {
+      const uint4 rv = *reinterpret_cast<const uint4*>(res + (int64_t)m * g.Ncols + c);
+      constexpr int E = 16 / (int)sizeof(T);
+      T a[E], b[E];
+      __builtin_memcpy(a, &v, 16);
+      __builtin_memcpy(b, &rv, 16);
+#pragma unroll
+      for (int e = 0; e < E; ++e) a[e] = p6::from_f<T>(p6::to_f(a[e]) + p6::to_f(b[e]));
+      __builtin_memcpy(&v, a, 16);
+    }
+    *reinterpret_cast<uint4*>(dst) = v;
+  }
+}
+
 template <typename T, int BM, int BN, int MODE>
 __global__ __launch_bounds__(kThreads) void conv_igemm_kernel(const T* __restrict__ src, const T* __restrict__ wts,
                                                               const float* __restrict__ bias, const T* __restrict__ res,
@@ -52,7 +152,6 @@ __global__ __launch_bounds__(kThreads) void conv_igemm_kernel(const T* __restric
   constexpr int A_PER = BM / 64;         // 16-B chunks per thread per A stage
   constexpr int B_PER = BN / 64;
   constexpr int STAGE = (BM + BN) * 64;  // bytes per LDS buffer
-  constexpr int CROW = BN * (int)sizeof(T) + 16;  // epilogue tile row stride (bytes)
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   // XCD-aware remap: consecutive logical tiles (same M rows) share an XCD's L2.
@@ -220,90 +319,202 @@ __global__ __launch_bounds__(kThreads) void conv_igemm_kernel(const T* __restric
     __syncthreads();
   }
 
-  // ---------------- epilogue ----------------
-  const int row_base = m0 + wm * (BM / 2);
-  const int col_base = n0 + wn * (BN / 2);
-  if (bias) {
+  conv_epilogue<T, BM, BN>(acc, smem, g, bias, res, out, stats, m0, n0);
+}
+
+// ============================================================================
+// Fast path (bf16, K a multiple of 64 within one tap): BK = 64, 3-stage LDS ring
+// filled by LDS-DMA (global_load_lds_dwordx4, 1 KiB = 8 rows x 128 B per wave
+// instruction), two stages in flight while the third is computed; one raw
+// s_barrier per K-step behind a counted vmcnt (never __syncthreads in the loop:
+// its fence would drain the in-flight DMA).  Padding taps / rows past M read a
+// zero page instead of being masked.  The XOR swizzle (row >> 1) & 7 is applied
+// on the DMA SOURCE address (the LDS destination of LDS-DMA is lane-linear) and
+// on the ds_read_b128 fragment reads: conflict-free for both 16-lane k-halves.
+// ============================================================================
+__device__ uint4 g_zero_page[4];   // 64 zero bytes (static storage: zero-initialised)
+
+__device__ __forceinline__ int swz8(int row) { return (row >> 1) & 7; }
+
+__device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
+                                   (void __attribute__((address_space(3)))*)lds_wave_base, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void vmcnt_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int MODE>
+__global__ __launch_bounds__(kThreads) void conv_lds3_kernel(const bf16* __restrict__ src, const bf16* __restrict__ wts,
+                                                             const float* __restrict__ bias,
+                                                             const bf16* __restrict__ res, bf16* __restrict__ out,
+                                                             float* __restrict__ stats, Geom g) {
+  constexpr int TM = BM / 32, TN = BN / 32;
+  constexpr int A_INS = BM / 32, B_INS = BN / 32;   // DMA instructions per thread per stage
+  constexpr int LOADS = A_INS + B_INS;
+  constexpr int SA = BM * 128, STAGE = (BM + BN) * 128;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nwg = g.gm * g.gn;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int tm = bid / g.gn, tn = bid - tm * g.gn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int r8 = lane >> 3, pch = lane & 7;
+  const char* zp = reinterpret_cast<const char*>(g_zero_page);
+
+  // rows this lane DMAs: row = i*32 + wave*8 + r8; it fetches logical chunk pch ^ swz8(row)
+  int a_pix[A_INS], a_y[A_INS], a_x[A_INS], a_ck[A_INS];
+  bool a_ok[A_INS];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int c = col_base + j * 16 + fr;
-      const float bv = c < g.Ncols ? bias[c] : 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) acc[i][j] += bv;
+  for (int i = 0; i < A_INS; ++i) {
+    const int row = i * 32 + wave * 8 + r8;
+    const int m = m0 + row;
+    a_ok[i] = m < g.M;
+    a_ck[i] = (pch ^ swz8(row)) * 8;
+    const int mm = a_ok[i] ? m : 0;
+    if (MODE == kGemm) {
+      a_pix[i] = mm; a_y[i] = 0; a_x[i] = 0;
+    } else {
+      const int hw = g.RH * g.RW;
+      const int n = mm / hw, rem = mm - n * hw;
+      const int y = rem / g.RW, x = rem - y * g.RW;
+      a_pix[i] = n * g.SH * g.SW;
+      if (MODE == kDgrad) { a_y[i] = y + g.pad; a_x[i] = x + g.pad; }
+      else { a_y[i] = y * g.stride - g.pad; a_x[i] = x * g.stride - g.pad; }
     }
   }
-  if (stats) {
-    // partials over blocks of 32 rows (two 16-row MFMA tiles), stats row = m / 32:
-    // (sum, M2 about the block-local mean) -- Chan-mergeable, free of the
-    // E[x^2]-E[x]^2 cancellation; row counts follow from M (pose6d_bn_finalize).
+  const bf16* b_src[B_INS];
 #pragma unroll
-    for (int h = 0; h < TM / 2; ++h) {
-      const int rb = row_base + h * 32;
-      const int nval = min(max(g.M - rb, 0), 32);
-      const float inv_n = nval > 0 ? 1.0f / (float)nval : 0.f;
+  for (int j = 0; j < B_INS; ++j) {
+    const int row = j * 32 + wave * 8 + r8;
+    const int n = n0 + row;
+    b_src[j] = n < g.Ncols ? wts + (int64_t)n * g.Kpad + (pch ^ swz8(row)) * 8 : nullptr;
+  }
+
+  auto issue = [&](int kt, int buf) {
+    const int k0 = kt * 64;
+    char* As = smem + buf * STAGE;
+    char* Bs = As + SA;
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        float s = 0.f;
+    for (int j = 0; j < B_INS; ++j)
+      glds16(b_src[j] ? (const void*)(b_src[j] + k0) : (const void*)zp, Bs + (j * 32 + wave * 8) * 128);
+    int kh = 0, kw = 0, c0 = k0;
+    if (MODE != kGemm) {
+      const int tap = k0 >> g.log2SC;
+      c0 = k0 & (g.SC - 1);
+      kh = tap / g.KW;
+      kw = tap - kh * g.KW;
+    }
 #pragma unroll
-        for (int i = 2 * h; i < 2 * h + 2; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int m = row_base + i * 16 + fc * 4 + r;
-            s += m < g.M ? acc[i][j][r] : 0.f;
-          }
-        s += __shfl_xor(s, 16, 64);
-        s += __shfl_xor(s, 32, 64);
-        const float mu = s * inv_n;
-        float q = 0.f;
-#pragma unroll
-        for (int i = 2 * h; i < 2 * h + 2; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int m = row_base + i * 16 + fc * 4 + r;
-            const float d = acc[i][j][r] - mu;
-            q = m < g.M ? fmaf(d, d, q) : q;
-          }
-        q += __shfl_xor(q, 16, 64);
-        q += __shfl_xor(q, 32, 64);
-        const int c = col_base + j * 16 + fr;
-        if (lane < 16 && c < g.Ncols && nval > 0) {
-          float* sp = stats + (int64_t)(rb >> 5) * 2 * g.Ncols;
-          sp[c] = s;
-          sp[g.Ncols + c] = q;
+    for (int i = 0; i < A_INS; ++i) {
+      const void* p = zp;
+      if (MODE == kGemm) {
+        if (a_ok[i]) p = src + (int64_t)a_pix[i] * g.K + k0 + a_ck[i];
+      } else {
+        int sy, sx;
+        bool ok = a_ok[i];
+        if (MODE == kFwd) {
+          sy = a_y[i] + kh; sx = a_x[i] + kw;
+        } else {
+          const int ty = a_y[i] - kh, tx = a_x[i] - kw;
+          ok = ok && ty >= 0 && tx >= 0;
+          if (g.stride == 2) { ok = ok && !(ty & 1) && !(tx & 1); sy = ty >> 1; sx = tx >> 1; }
+          else { sy = ty; sx = tx; }
         }
+        ok = ok && (unsigned)sy < (unsigned)g.SH && (unsigned)sx < (unsigned)g.SW;
+        if (ok) p = src + ((int64_t)(a_pix[i] + sy * g.SW + sx) << g.log2SC) + c0 + a_ck[i];
       }
+      glds16(p, As + (i * 32 + wave * 8) * 128);
     }
-  }
-  // stage the tile through LDS (staging buffers are dead after the final barrier)
+  };
+
+  f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fc = lane >> 4;
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + SA;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int lr = wm * (BM / 2) + i * 16 + fc * 4 + r;
-        const int lc = wn * (BN / 2) + j * 16 + fr;
-        *reinterpret_cast<T*>(smem + lr * CROW + lc * (int)sizeof(T)) = p6::from_f<T>(acc[i][j][r]);
+    for (int kk = 0; kk < 2; ++kk) {
+      uint4 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * (BM / 2) + i * 16 + fr;
+        af[i] = *reinterpret_cast<const uint4*>(As + row * 128 + (((fc + 4 * kk) ^ swz8(row)) << 4));
       }
-  __syncthreads();
-  constexpr int CPR = BN * (int)sizeof(T) / 16;  // 16-B chunks per tile row
-  for (int idx = tid; idx < BM * CPR; idx += kThreads) {
-    const int lr = idx / CPR, cc = idx - lr * CPR;
-    const int m = m0 + lr, c = n0 + cc * (16 / (int)sizeof(T));
-    if (m >= g.M || c >= g.Ncols) continue;
-    uint4 v = *reinterpret_cast<const uint4*>(smem + lr * CROW + cc * 16);
-    T* dst = out + (int64_t)m * g.Ncols + c;
-    if (res) {
-      const uint4 rv = *reinterpret_cast<const uint4*>(res + (int64_t)m * g.Ncols + c);
-      constexpr int E = 16 / (int)sizeof(T);
-      T a[E], b[E];
-      __builtin_memcpy(a, &v, 16);
-      __builtin_memcpy(b, &rv, 16);
 #pragma unroll
-      for (int e = 0; e < E; ++e) a[e] = p6::from_f<T>(p6::to_f(a[e]) + p6::to_f(b[e]));
-      __builtin_memcpy(&v, a, 16);
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * (BN / 2) + j * 16 + fr;
+        bfr[j] = *reinterpret_cast<const uint4*>(Bs + row * 128 + (((fc + 4 * kk) ^ swz8(row)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
+                                                              __builtin_bit_cast(bf16x8, bfr[j]), acc[i][j], 0, 0, 0);
     }
-    *reinterpret_cast<uint4*>(dst) = v;
+  };
+
+  const int nk = g.Kpad / 64;
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) vmcnt_barrier<LOADS>();   // stage kt landed (kt+1 may still fly)
+    else vmcnt_barrier<0>();
+    if (kt + 2 < nk) issue(kt + 2, cur == 0 ? 2 : cur - 1);   // the buffer computed at kt-1
+    compute(cur);
+    cur = cur == 2 ? 0 : cur + 1;
+  }
+  asm volatile("s_barrier" ::: "memory");   // every wave done reading the ring before the epilogue reuses it
+  conv_epilogue<bf16, BM, BN>(acc, smem, g, bias, res, out, stats, m0, n0);
+}
+
+template <int BM, int BN, int MODE>
+int launch_fast(const Geom& g0, const void* src, const void* w, const float* bias, const void* res, void* out,
+                float* stats, hipStream_t s) {
+  Geom g = g0;
+  g.gm = p6::ceil_div(g.M, BM);
+  g.gn = p6::ceil_div(g.Ncols, BN);
+  const int ring = 3 * (BM + BN) * 128;
+  const int epi = BM * (BN * 2 + 16);
+  const int lds = ring > epi ? ring : epi;
+  conv_lds3_kernel<BM, BN, MODE><<<g.gm * g.gn, kThreads, lds, s>>>((const bf16*)src, (const bf16*)w, bias,
+                                                                     (const bf16*)res, (bf16*)out, stats, g);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+template <int MODE>
+int launch_fast_mode(const Geom& g, int tile, const void* src, const void* w, const float* bias, const void* res,
+                     void* out, float* stats, hipStream_t s) {
+  switch (tile) {
+    case 0: return launch_fast<128, 128, MODE>(g, src, w, bias, res, out, stats, s);
+    case 1: return launch_fast<128, 64, MODE>(g, src, w, bias, res, out, stats, s);
+    case 2: return launch_fast<64, 128, MODE>(g, src, w, bias, res, out, stats, s);
+    default: return launch_fast<64, 64, MODE>(g, src, w, bias, res, out, stats, s);
+  }
+}
+
+int dispatch_fast(int mode, const Geom& g, int tile, const void* src, const void* w, const float* bias,
+                  const void* res, void* out, float* stats, hipStream_t s) {
+  switch (mode) {
+    case kGemm: return launch_fast_mode<kGemm>(g, tile, src, w, bias, res, out, stats, s);
+    case kFwd: return launch_fast_mode<kFwd>(g, tile, src, w, bias, res, out, stats, s);
+    default: return launch_fast_mode<kDgrad>(g, tile, src, w, bias, res, out, stats, s);
   }
 }
 
@@ -360,13 +571,78 @@ int dispatch(int mode, const Geom& g, int tile, const void* src, const void* w, 
   }
 }
 
-}  // namespace
+
 
 // statistics rows: one per 32 output pixels (the last may cover fewer)
 extern "C" int pose6d_conv_stats_rows(int32_t N, int32_t Ho, int32_t Wo, int32_t Cout) {
   (void)Cout;
   return p6::ceil_div((int64_t)N * Ho * Wo, 32);
 }
+
+// implementation choice: the LDS-DMA fast path for bf16 whenever each 64-deep K slice
+// lies inside one filter tap; the register-staged kernel otherwise (fp32, stem,
+// 32-channel z-CNN).  POSE6D_CONV_IMPL=base|fast and POSE6D_CONV_TILE=0..3 override
+// (tuning / A-B experiments only).
+bool fast_ok(int dtype, int mode, const Geom& g) {
+  if (dtype != POSE6D_DT_BF16 || mode == kFwdNarrow) return false;
+  if (g.K % 64 != 0 || g.Kpad != g.K) return false;
+  return mode == kGemm || g.SC % 64 == 0;
+}
+
+int pick_tile_fast(int M, int N) {
+  auto blocks = [&](int bm, int bn) { return (int64_t)p6::ceil_div(M, bm) * p6::ceil_div(N, bn); };
+  if (N <= 64) return blocks(128, 64) >= 256 ? 1 : 3;
+  if (blocks(128, 128) >= 256) return 0;
+  if (blocks(128, 64) >= 256) return 1;
+  return 3;
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
+
+int choose(int dtype, int mode, const Geom& g, bool* fast) {
+  const char* impl = getenv("POSE6D_CONV_IMPL");
+  *fast = fast_ok(dtype, mode, g) && !(impl && strcmp(impl, "base") == 0);
+  const int t = *fast ? pick_tile_fast(g.M, g.Ncols) : pick_tile(g.M, g.Ncols);
+  return env_int("POSE6D_CONV_TILE", t);
+}
+
+int run_conv(int dtype, int mode, const Geom& g, const void* src, const void* w, const float* bias, const void* res,
+             void* out, float* stats, hipStream_t s) {
+  bool fast;
+  const int tile = choose(dtype, mode, g, &fast);
+  if (fast) return dispatch_fast(mode, g, tile, src, w, bias, res, out, stats, s);
+  return dtype == POSE6D_DT_BF16 ? dispatch<bf16>(mode, g, tile, src, w, bias, res, out, stats, s)
+                                 : dispatch<float>(mode, g, tile, src, w, bias, res, out, stats, s);
+}
+
+Geom fwd_geom(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad, int Ho, int Wo,
+              int* mode) {
+  const int bk = dtype == POSE6D_DT_BF16 ? 32 : 16;
+  Geom g{};
+  g.M = N * Ho * Wo; g.Ncols = Cout; g.K = KH * KW * Cin;
+  g.Kpad = p6::ceil_div(g.K, bk) * bk;
+  g.SH = H; g.SW = W; g.SC = Cin; g.log2SC = ilog2(Cin); g.RH = Ho; g.RW = Wo;
+  g.KH = KH; g.KW = KW; g.stride = stride; g.pad = pad;
+  if (KH == 1 && KW == 1 && stride == 1 && pad == 0) *mode = kGemm;
+  else if (Cin == 4) *mode = kFwdNarrow;
+  else *mode = kFwd;
+  return g;
+}
+
+Geom dgrad_geom(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad, int Ho, int Wo,
+                int* mode) {
+  Geom g{};
+  g.M = N * H * W; g.Ncols = Cin; g.K = KH * KW * Cout; g.Kpad = g.K;
+  g.SH = Ho; g.SW = Wo; g.SC = Cout; g.log2SC = ilog2(Cout); g.RH = H; g.RW = W;
+  g.KH = KH; g.KW = KW; g.stride = stride; g.pad = pad;
+  *mode = (KH == 1 && KW == 1 && stride == 1 && pad == 0) ? kGemm : kDgrad;
+  return g;
+}
+
+}  // namespace
 
 extern "C" int pose6d_conv2d_fwd(int32_t dtype, const void* x, const void* w, const float* bias, void* y,
                                  float* stats, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH,
@@ -376,24 +652,13 @@ extern "C" int pose6d_conv2d_fwd(int32_t dtype, const void* x, const void* w, co
   P6_CHECK_ARG(Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1,
                "pose6d_conv2d_fwd: Ho/Wo inconsistent");
   const int bk = dtype == POSE6D_DT_BF16 ? 32 : 16;
-  const int lc = ilog2(Cin);
-  Geom g{};
-  g.M = N * Ho * Wo; g.Ncols = Cout; g.K = KH * KW * Cin;
-  g.Kpad = p6::ceil_div(g.K, bk) * bk;
-  g.SH = H; g.SW = W; g.SC = Cin; g.log2SC = lc; g.RH = Ho; g.RW = Wo;
-  g.KH = KH; g.KW = KW; g.stride = stride; g.pad = pad;
   int mode;
-  if (KH == 1 && KW == 1 && stride == 1 && pad == 0) mode = kGemm;
-  else if (Cin == 4) mode = kFwdNarrow;
-  else {
-    P6_CHECK_ARG(lc >= 0 && Cin % bk == 0, "pose6d_conv2d_fwd: Cin must be 4 or a power of two >= %d (got %d)", bk, Cin);
-    mode = kFwd;
-  }
+  const Geom g = fwd_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
+  if (mode == kFwd)
+    P6_CHECK_ARG(g.log2SC >= 0 && Cin % bk == 0, "pose6d_conv2d_fwd: Cin must be 4 or a power of two >= %d (got %d)",
+                 bk, Cin);
   if (mode == kGemm) P6_CHECK_ARG(Cin % bk == 0, "pose6d_conv2d_fwd: 1x1 Cin %% %d != 0", bk);
-  const int tile = pick_tile(g.M, Cout);
-  hipStream_t s = p6::stream_of(stream);
-  return dtype == POSE6D_DT_BF16 ? dispatch<bf16>(mode, g, tile, x, w, bias, nullptr, y, stats, s)
-                                 : dispatch<float>(mode, g, tile, x, w, bias, nullptr, y, stats, s);
+  return run_conv(dtype, mode, g, x, w, bias, nullptr, y, stats, p6::stream_of(stream));
 }
 
 extern "C" int pose6d_conv2d_dgrad(int32_t dtype, const void* dy, const void* wt, const void* dres, void* dx,
@@ -403,26 +668,21 @@ extern "C" int pose6d_conv2d_dgrad(int32_t dtype, const void* dy, const void* wt
   P6_CHECK_ARG(stride == 1 || stride == 2, "pose6d_conv2d_dgrad: stride must be 1 or 2");
   P6_CHECK_ARG(Cin % 8 == 0, "pose6d_conv2d_dgrad: Cin %% 8 != 0 (no data gradient for the stem)");
   const int bk = dtype == POSE6D_DT_BF16 ? 32 : 16;
-  const int lc = ilog2(Cout);
-  P6_CHECK_ARG(lc >= 0 && Cout % bk == 0, "pose6d_conv2d_dgrad: Cout must be a power of two >= %d", bk);
-  Geom g{};
-  g.M = N * H * W; g.Ncols = Cin; g.K = KH * KW * Cout; g.Kpad = g.K;
-  g.SH = Ho; g.SW = Wo; g.SC = Cout; g.log2SC = lc; g.RH = H; g.RW = W;
-  g.KH = KH; g.KW = KW; g.stride = stride; g.pad = pad;
-  const int mode = (KH == 1 && KW == 1 && stride == 1 && pad == 0) ? kGemm : kDgrad;
-  const int tile = pick_tile(g.M, Cin);
-  hipStream_t s = p6::stream_of(stream);
-  return dtype == POSE6D_DT_BF16 ? dispatch<bf16>(mode, g, tile, dy, wt, nullptr, dres, dx, nullptr, s)
-                                 : dispatch<float>(mode, g, tile, dy, wt, nullptr, dres, dx, nullptr, s);
+  int mode;
+  const Geom g = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
+  P6_CHECK_ARG(g.log2SC >= 0 && Cout % bk == 0, "pose6d_conv2d_dgrad: Cout must be a power of two >= %d", bk);
+  return run_conv(dtype, mode, g, dy, wt, nullptr, dres, dx, nullptr, p6::stream_of(stream));
 }
 
-// launch variant of a forward / data-gradient conv: (mode << 4) | tile, with tile
-// 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64 (for profiling / roofline joins)
-extern "C" int pose6d_conv_variant(int32_t pass, int32_t M, int32_t Ncols, int32_t KH, int32_t KW, int32_t stride,
-                                   int32_t pad, int32_t Cin) {
+// launch variant of a forward / data-gradient conv, for profiling joins:
+// (fast << 8) | (mode << 4) | tile, tile 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64
+extern "C" int pose6d_conv_variant(int32_t dtype, int32_t pass, int32_t N, int32_t H, int32_t W, int32_t Cin,
+                                   int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho,
+                                   int32_t Wo) {
   int mode;
-  if (KH == 1 && KW == 1 && stride == 1 && pad == 0) mode = kGemm;
-  else if (pass == 0) mode = Cin == 4 ? kFwdNarrow : kFwd;
-  else mode = kDgrad;
-  return (mode << 4) | pick_tile(M, Ncols);
+  const Geom g = pass == 0 ? fwd_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode)
+                           : dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
+  bool fast;
+  const int tile = choose(dtype, mode, g, &fast);
+  return ((int)fast << 8) | (mode << 4) | tile;
 }

@@ -14,6 +14,14 @@ def _tname(dtype):
     return "__bf16" if dtype == torch.bfloat16 else "float"
 
 
+def _sym(v, T):
+    bm, bn = TILES[v & 15]
+    mode = (v >> 4) & 15
+    if (v >> 8) & 1:
+        return f"conv_lds3_kernel<{bm}, {bn}, {mode}>"
+    return f"conv_igemm_kernel<{T}, {bm}, {bn}, {mode}>"
+
+
 def conv_launches(eng):
     """(symbol, flops, launch-callable) for every conv pass of one training step."""
     B, dt, T = eng.B, eng.dt, _tname(eng.dtype)
@@ -23,19 +31,16 @@ def conv_launches(eng):
         M = B * op.Ho * op.Wo
         K = op.k * op.k * op.cin
         flops = 2.0 * M * op.cout * K
-        v = query("conv_variant", 0, M, op.cout, op.k, op.k, op.stride, op.pad, op.cin_pad)
-        bm, bn = TILES[v & 15]
-        sym = f"conv_igemm_kernel<{T}, {bm}, {bn}, {v >> 4}>"
+        sym = _sym(query("conv_variant", dt, 0, B, op.H, op.W, op.cin_pad, op.cout, op.k, op.k, op.stride, op.pad,
+                         op.Ho, op.Wo), T)
 
         def fwd(op=op):
             call("conv2d_fwd", dt, op.src.t, op.wp, op.conv.bias, op.out.t, op.stats, B, op.H, op.W, op.cin_pad,
                  op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, st)
         out.append((sym, flops, fwd, op.name + ".fwd"))
         if op.needs_dgrad:
-            Md = B * op.H * op.W
-            v = query("conv_variant", 1, Md, op.cin_pad, op.k, op.k, op.stride, op.pad, op.cin_pad)
-            bm, bn = TILES[v & 15]
-            sym = f"conv_igemm_kernel<{T}, {bm}, {bn}, {v >> 4}>"
+            sym = _sym(query("conv_variant", dt, 1, B, op.H, op.W, op.cin_pad, op.cout, op.k, op.k, op.stride,
+                             op.pad, op.Ho, op.Wo), T)
 
             def dgrad(op=op):
                 call("conv2d_dgrad", dt, op.out.g, op.wt, None, op.dres, B, op.H, op.W, op.cin_pad, op.cout, op.k,

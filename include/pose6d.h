@@ -124,10 +124,11 @@ int pose6d_conv2d_fwd(int32_t dtype, const void *x, const void *wp, const float 
                       int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW,
                       int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, void *stream);
 /* kernel variant a conv launch selects (profiling joins): fwd/dgrad (pass 0/1):
- * (mode << 4) | tile (tile 0..3 = 128x128, 128x64, 64x128, 64x64; mode 0 gemm,
- * 1 im2col, 2 narrow stem, 3 dgrad); wgrad: (BM == 128) << 1 | (BN == 128). */
-int pose6d_conv_variant(int32_t pass, int32_t M, int32_t Ncols, int32_t KH, int32_t KW, int32_t stride,
-                        int32_t pad, int32_t Cin);
+ * (fast << 8) | (mode << 4) | tile (tile 0..3 = 128x128, 128x64, 64x128, 64x64;
+ * mode 0 gemm, 1 im2col, 2 narrow stem, 3 dgrad; fast = LDS-DMA bf16 kernel);
+ * wgrad: (BM == 128) << 1 | (BN == 128). */
+int pose6d_conv_variant(int32_t dtype, int32_t pass, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout,
+                        int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo);
 int pose6d_wgrad_variant(int32_t dtype, int32_t M, int32_t Cout, int32_t K);
 /* data gradient: dx [N][H][W][Cin] = conv_transpose(dy [N][Ho][Wo][Cout], wt) (+ dres if non-NULL) */
 int pose6d_conv2d_dgrad(int32_t dtype, const void *dy, const void *wt, const void *dres, void *dx, int32_t N,
