@@ -183,67 +183,56 @@ __global__ __launch_bounds__(kThreads) void bn_act_kernel(const T* __restrict__ 
 }
 
 // ---------------------------------------------------------------- backward
-// Each block: ROWS_PER_BLOCK rows x all channels; thread = (row lane, channel chunk).
+// grid (channel-chunk groups, row blocks): block = CL chunk-lanes (consecutive 16-B
+// chunks of a row: coalesced) x RL row-lanes; partial row = blockIdx.y.
 template <typename T>
-__global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __restrict__ dout, const T* __restrict__ out,
-                                                                 const T* __restrict__ y, const float* __restrict__ mean,
-                                                                 const float* __restrict__ inv, float* __restrict__ part,
-                                                                 int64_t M, int C, int rows_per_block) {
+__global__ __launch_bounds__(kThreads) void bn_bwd_reduce2_kernel(const T* __restrict__ dout, const T* __restrict__ out,
+                                                                  const T* __restrict__ y,
+                                                                  const float* __restrict__ mean,
+                                                                  const float* __restrict__ inv,
+                                                                  float* __restrict__ part, int64_t M, int C,
+                                                                  int rows_per_block) {
   constexpr int E = V<T>::E;
-  extern __shared__ float sred[];  // [kThreads][2*E]
+  __shared__ float sred[kThreads][2 * E + 1];
   const int cpr = C / E;
-  const int tpr = kThreads / cpr > 0 ? kThreads / cpr : 1;  // threads along rows
-  const int cc = threadIdx.x % cpr, rl = threadIdx.x / cpr;
-  float s[E], q[E];
-  // channel chunks beyond kThreads are looped (then tpr == 1: no cross-thread reduce)
-  for (int ch = cc; ch < cpr; ch += kThreads) {
+  const int CL = cpr < 64 ? cpr : 64, RL = kThreads / CL;
+  const int cl = threadIdx.x % CL, rl = threadIdx.x / CL;
+  const int ch = blockIdx.x * CL + cl;
+  const int c0 = ch * E;
+  float s[E], q[E], mu[E], iv[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) s[e] = q[e] = 0.f;
-    const int c0 = ch * E;
-    float mu[E], iv[E];
+  for (int e = 0; e < E; ++e) { s[e] = q[e] = 0.f; mu[e] = mean[c0 + e]; iv[e] = inv[c0 + e]; }
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  for (int64_t r = r0 + rl; r < r1; r += RL) {
+    const int64_t off = r * C + c0;
+    float d[E], yy[E];
+    load_vec(dout + off, d);
+    if (out) {
+      float o[E];
+      load_vec(out + off, o);
 #pragma unroll
-    for (int e = 0; e < E; ++e) { mu[e] = mean[c0 + e]; iv[e] = inv[c0 + e]; }
-    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
-    const int64_t r1 = min(M, r0 + rows_per_block);
-    if (rl < tpr)
-      for (int64_t r = r0 + rl; r < r1; r += tpr) {
-        const int64_t off = r * C + c0;
-        float d[E], yy[E];
-        load_vec(dout + off, d);
-        if (out) {
-          float o[E];
-          load_vec(out + off, o);
-#pragma unroll
-          for (int e = 0; e < E; ++e) d[e] = o[e] > 0.f ? d[e] : 0.f;
-        }
-        load_vec(y + off, yy);
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          s[e] += d[e];
-          q[e] = fmaf(d[e], (yy[e] - mu[e]) * iv[e], q[e]);
-        }
-      }
-    // reduce over the tpr row-threads sharing this chunk
-    if (cpr <= kThreads) {
-#pragma unroll
-      for (int e = 0; e < E; ++e) { sred[threadIdx.x * 2 * E + e] = s[e]; sred[threadIdx.x * 2 * E + E + e] = q[e]; }
-      __syncthreads();
-      if (rl == 0) {
-        for (int k = 1; k < tpr; ++k) {
-          const int t = k * cpr + cc;
-#pragma unroll
-          for (int e = 0; e < E; ++e) { s[e] += sred[t * 2 * E + e]; q[e] += sred[t * 2 * E + E + e]; }
-        }
-        float* pp = part + (int64_t)blockIdx.x * 2 * C;
-#pragma unroll
-        for (int e = 0; e < E; ++e) { pp[c0 + e] = s[e]; pp[C + c0 + e] = q[e]; }
-      }
-      __syncthreads();
-    } else {
-      float* pp = part + (int64_t)blockIdx.x * 2 * C;
-#pragma unroll
-      for (int e = 0; e < E; ++e) { pp[c0 + e] = s[e]; pp[C + c0 + e] = q[e]; }
+      for (int e = 0; e < E; ++e) d[e] = o[e] > 0.f ? d[e] : 0.f;
     }
+    load_vec(y + off, yy);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      s[e] += d[e];
+      q[e] = fmaf(d[e], (yy[e] - mu[e]) * iv[e], q[e]);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) { sred[threadIdx.x][e] = s[e]; sred[threadIdx.x][E + e] = q[e]; }
+  __syncthreads();
+  if (rl == 0) {
+    for (int k = 1; k < RL; ++k) {
+      const int t = k * CL + cl;
+#pragma unroll
+      for (int e = 0; e < E; ++e) { s[e] += sred[t][e]; q[e] += sred[t][E + e]; }
+    }
+    float* pp = part + (int64_t)blockIdx.y * 2 * C;
+#pragma unroll
+    for (int e = 0; e < E; ++e) { pp[c0 + e] = s[e]; pp[C + c0 + e] = q[e]; }
   }
 }
 
@@ -343,9 +332,9 @@ inline unsigned grid_for(int64_t chunks) {
 }
 
 int rows_per_block(int64_t M) {
-  // ~256 blocks of work, at least 64 rows each
+  // up to 256 row blocks (x the channel-chunk groups), at least 16 rows each
   int64_t r = (M + 255) / 256;
-  if (r < 64) r = 64;
+  if (r < 16) r = 16;
   return (int)r;
 }
 
@@ -396,12 +385,17 @@ extern "C" int pose6d_bn_bwd(int32_t dtype, const void* dout, const void* out, c
   const int nb = p6::ceil_div(M, rpb);
   float* part = workspace;                          // [nb][2][C]
   float* coef = workspace + (int64_t)nb * 2 * C;    // [3][C]
+  const int E = dtype == POSE6D_DT_BF16 ? 8 : 4;
+  const int cpr = C / E;
+  const int cl = cpr < 64 ? cpr : 64;
+  P6_CHECK_ARG(cpr % cl == 0 && kThreads % cl == 0, "pose6d_bn_bwd: C / vector width must be a power of two");
+  dim3 grid(cpr / cl, nb);
   if (dtype == POSE6D_DT_BF16) {
-    bn_bwd_reduce_kernel<bf16><<<nb, kThreads, kThreads * 2 * 8 * 4, s>>>(
-        (const bf16*)dout, (const bf16*)out, (const bf16*)y, mean, invstd, part, M, C, rpb);
+    bn_bwd_reduce2_kernel<bf16><<<grid, kThreads, 0, s>>>((const bf16*)dout, (const bf16*)out, (const bf16*)y, mean,
+                                                          invstd, part, M, C, rpb);
   } else {
-    bn_bwd_reduce_kernel<float><<<nb, kThreads, kThreads * 2 * 4 * 4, s>>>(
-        (const float*)dout, (const float*)out, (const float*)y, mean, invstd, part, M, C, rpb);
+    bn_bwd_reduce2_kernel<float><<<grid, kThreads, 0, s>>>((const float*)dout, (const float*)out, (const float*)y, mean,
+                                                           invstd, part, M, C, rpb);
   }
   P6_LAUNCH_CHECK();
   bn_bwd_finalize_kernel<<<p6::ceil_div(C, 16), kThreads, 0, s>>>(part, nb, C, (double)M, gamma, invstd, dgamma, dbeta,

@@ -1,0 +1,97 @@
+"""Per-layer conv timing sweep (GPU box): every distinct ResNet50 conv shape at
+batch 32 bf16, fwd / dgrad / wgrad, each implementation x tile, TFLOP/s.
+usage: python tools/conv_bench.py [--passes fwd,dgrad] [--impls base,fast] [--tiles 0,1,2,3]"""
+import argparse
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "6d-pose-estimation_amd")]
+
+from pose6d._lib import call, query, stream  # noqa: E402
+from pose6d.trunk import DTYPES, pack_single  # noqa: E402
+
+# (H, W, Cin, Cout, k, s, p) per distinct ResNet50 conv (input geometry)
+SHAPES = [
+    (56, 56, 64, 64, 1, 1, 0), (56, 56, 64, 64, 3, 1, 1), (56, 56, 64, 256, 1, 1, 0), (56, 56, 256, 64, 1, 1, 0),
+    (56, 56, 256, 128, 1, 1, 0), (56, 56, 128, 128, 3, 2, 1), (28, 28, 128, 512, 1, 1, 0), (56, 56, 256, 512, 1, 2, 0),
+    (28, 28, 512, 128, 1, 1, 0), (28, 28, 128, 128, 3, 1, 1), (28, 28, 512, 256, 1, 1, 0),
+    (28, 28, 256, 256, 3, 2, 1), (14, 14, 256, 1024, 1, 1, 0), (28, 28, 512, 1024, 1, 2, 0),
+    (14, 14, 1024, 256, 1, 1, 0), (14, 14, 256, 256, 3, 1, 1), (14, 14, 1024, 512, 1, 1, 0),
+    (14, 14, 512, 512, 3, 2, 1), (7, 7, 512, 2048, 1, 1, 0), (14, 14, 1024, 2048, 1, 2, 0),
+    (7, 7, 2048, 512, 1, 1, 0), (7, 7, 512, 512, 3, 1, 1),
+]
+
+
+def timeit(fn, reps=20):
+    fn()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        fn()
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--passes", default="fwd,dgrad,wgrad")
+    ap.add_argument("--impls", default="base,fast")
+    ap.add_argument("--tiles", default="auto,0,1,3")
+    ap.add_argument("--B", type=int, default=32)
+    a = ap.parse_args()
+    B, dt, dtype, dev = a.B, DTYPES[torch.bfloat16], torch.bfloat16, "cuda"
+    st = stream()
+    tot = {}
+    for (H, W, Cin, Cout, k, s, p) in SHAPES:
+        Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        x = torch.randn(B, H, W, Cin, device=dev).to(dtype)
+        w = torch.randn(Cout, Cin, k, k, device=dev) * 0.05
+        wp, wt = pack_single(w, Cin, dtype)
+        y = torch.empty(B, Ho, Wo, Cout, device=dev, dtype=dtype)
+        dy = torch.randn(B, Ho, Wo, Cout, device=dev).to(dtype)
+        dx = torch.empty(B, H, W, Cin, device=dev, dtype=dtype)
+        stats = torch.empty(query("conv_stats_rows", B, Ho, Wo, Cout), 2, Cout, device=dev)
+        ws = torch.empty(query("conv2d_wgrad_workspace", dt, B, Ho, Wo, Cin, Cout, k, k) // 4 + 1, device=dev)
+        dw = torch.empty(Cout, Cin, k, k, device=dev)
+        flops = 2.0 * B * Ho * Wo * Cout * Cin * k * k
+        fns = {
+            "fwd": lambda: call("conv2d_fwd", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, st),
+            "dgrad": lambda: call("conv2d_dgrad", dt, dy, wt, None, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, st),
+            "wgrad": lambda: call("conv2d_wgrad", dt, x, dy, dw, 0, ws, B, H, W, Cin, Cin, Cout, k, k, s, p, Ho, Wo,
+                                  st),
+        }
+        line = f"{H:3d}x{W:<3d} {Cin:4d}->{Cout:<4d} k{k}s{s} |"
+        for ps in a.passes.split(","):
+            impls = a.impls.split(",") if ps != "wgrad" else ["base"]
+            tiles = a.tiles.split(",") if ps != "wgrad" else ["auto"]
+            best = None
+            for impl in impls:
+                for t in tiles:
+                    os.environ["POSE6D_CONV_IMPL"] = impl
+                    if t == "auto":
+                        os.environ.pop("POSE6D_CONV_TILE", None)
+                    else:
+                        os.environ["POSE6D_CONV_TILE"] = t
+                    try:
+                        sec = timeit(fns[ps])
+                    except Exception as e:  # noqa: BLE001
+                        line += f" {ps}:{impl}/{t}=ERR"
+                        continue
+                    tf = flops / sec / 1e12
+                    line += f" {ps[0]}{impl[0]}{t}:{sec * 1e6:6.1f}us/{tf:5.0f}T"
+                    if t == "auto":
+                        tot[(ps, impl)] = tot.get((ps, impl), 0.0) + sec
+        os.environ.pop("POSE6D_CONV_IMPL", None)
+        os.environ.pop("POSE6D_CONV_TILE", None)
+        print(line, flush=True)
+    print("totals (auto tile, one instance per distinct shape):",
+          {f"{k[0]}/{k[1]}": round(v * 1e3, 3) for k, v in tot.items()})
+
+
+if __name__ == "__main__":
+    main()
