@@ -30,7 +30,10 @@ template <typename T> struct KT;
 template <> struct KT<bf16> { static constexpr int VEC = 8; static constexpr int BK = 32; };
 template <> struct KT<float> { static constexpr int VEC = 4; static constexpr int BK = 16; };
 
-enum Mode { kGemm = 0, kFwd = 1, kFwdNarrow = 2, kDgrad = 3 };
+// kDgradS2: stride-2 data gradient split into the four output parity classes
+// (y & 1, x & 1); each class only gathers the taps that reach it, so no MAC is
+// spent on the zeros a masked stride-2 gather would multiply.
+enum Mode { kGemm = 0, kFwd = 1, kFwdNarrow = 2, kDgrad = 3, kDgradS2 = 4 };
 
 struct Geom {
   int M, Ncols, K, Kpad;   // GEMM dims; Kpad = weight row length
@@ -44,12 +47,23 @@ struct Geom {
 // block; this XOR makes every 16-lane LDS group hit 16 distinct 16-byte slots.
 __device__ __forceinline__ int swz(int row) { return (4 - ((row >> 2) & 3)) & 3; }
 
+// Output row of GEMM row m: m itself, or for a kDgradS2 parity class cls = (py, px)
+// the dX pixel (n, 2*yy + py, 2*xx + px) of class-local row m = (n, yy, xx).
+__device__ __forceinline__ int64_t out_row(const Geom& g, int cls, int m) {
+  if (cls < 0) return m;
+  const int hw = g.RH * g.RW;
+  const int n = m / hw, rem = m - n * hw;
+  const int yy = rem / g.RW, xx = rem - yy * g.RW;
+  return ((int64_t)n * 2 * g.RH + 2 * yy + (cls >> 1)) * (2 * g.RW) + 2 * xx + (cls & 1);
+}
+
 // Shared epilogue: + bias, BatchNorm partial statistics, LDS-staged 16-B stores
 // (+ residual).  Must be entered after a barrier that ends all LDS reads.
 template <typename T, int BM, int BN>
 __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const Geom& g,
                                               const float* __restrict__ bias, const T* __restrict__ res,
-                                              T* __restrict__ out, float* __restrict__ stats, int m0, int n0) {
+                                              T* __restrict__ out, float* __restrict__ stats, int m0, int n0,
+                                              int cls = -1) {
   constexpr int TM = BM / 32, TN = BN / 32;
   constexpr int CROW = BN * (int)sizeof(T) + 16;  // epilogue tile row stride (bytes)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -126,9 +140,10 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], ch
     const int m = m0 + lr, c = n0 + cc * (16 / (int)sizeof(T));
     if (m >= g.M || c >= g.Ncols) continue;
     uint4 v = *reinterpret_cast<const uint4*>(smem + lr * CROW + cc * 16);
-    T* dst = out + (int64_t)m * g.Ncols + c;
+    const int64_t om = out_row(g, cls, m);
+    T* dst = out + om * g.Ncols + c;
     if (res) {
-      const uint4 rv = *reinterpret_cast<const uint4*>(res + (int64_t)m * g.Ncols + c);
+      const uint4 rv = *reinterpret_cast<const uint4*>(res + om * g.Ncols + c);
       constexpr int E = 16 / (int)sizeof(T);
       T a[E], b[E];
       __builtin_memcpy(a, &v, 16);
@@ -323,14 +338,16 @@ __global__ __launch_bounds__(kThreads) void conv_igemm_kernel(const T* __restric
 }
 
 // ============================================================================
-// Fast path (bf16, K a multiple of 64 within one tap): BK = 64, 3-stage LDS ring
-// filled by LDS-DMA (global_load_lds_dwordx4, 1 KiB = 8 rows x 128 B per wave
-// instruction), two stages in flight while the third is computed; one raw
+// Fast path (bf16, K a multiple of 64 within one tap): BK = 64, an S-stage LDS
+// ring filled by LDS-DMA (global_load_lds_dwordx4, 1 KiB = 8 rows x 128 B per
+// wave instruction), S-1 stages in flight while one is computed; one raw
 // s_barrier per K-step behind a counted vmcnt (never __syncthreads in the loop:
 // its fence would drain the in-flight DMA).  Padding taps / rows past M read a
 // zero page instead of being masked.  The XOR swizzle (row >> 1) & 7 is applied
 // on the DMA SOURCE address (the LDS destination of LDS-DMA is lane-linear) and
 // on the ds_read_b128 fragment reads: conflict-free for both 16-lane k-halves.
+// S is picked per layer: deep rings for small, long-K grids (latency bound: one
+// workgroup per CU, each K-step short), shallow ones for big grids (occupancy).
 // ============================================================================
 __device__ uint4 g_zero_page[4];   // 64 zero bytes (static storage: zero-initialised)
 
@@ -343,25 +360,51 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
 
 template <int N>
 __device__ __forceinline__ void vmcnt_barrier() {
+  static_assert(N >= 0 && N < 64, "vmcnt is a 6-bit count");
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, int MODE>
-__global__ __launch_bounds__(kThreads) void conv_lds3_kernel(const bf16* __restrict__ src, const bf16* __restrict__ wts,
-                                                             const float* __restrict__ bias,
-                                                             const bf16* __restrict__ res, bf16* __restrict__ out,
-                                                             float* __restrict__ stats, Geom g) {
+// wait until at most `ahead` stages (LOADS DMA instructions each) are still in
+// flight, then barrier; `ahead` is wave-uniform, J the largest value it takes
+template <int LOADS, int J>
+__device__ __forceinline__ void wait_ahead(int ahead) {
+  if constexpr (J <= 0) {
+    vmcnt_barrier<0>();
+  } else {
+    if (ahead >= J) vmcnt_barrier<J * LOADS>();
+    else wait_ahead<LOADS, J - 1>(ahead);
+  }
+}
+
+template <int BM, int BN, int MODE, int S>
+__global__ __launch_bounds__(kThreads) void conv_lds_kernel(const bf16* __restrict__ src, const bf16* __restrict__ wts,
+                                                            const float* __restrict__ bias,
+                                                            const bf16* __restrict__ res, bf16* __restrict__ out,
+                                                            float* __restrict__ stats, Geom g) {
   constexpr int TM = BM / 32, TN = BN / 32;
   constexpr int A_INS = BM / 32, B_INS = BN / 32;   // DMA instructions per thread per stage
   constexpr int LOADS = A_INS + B_INS;
   constexpr int SA = BM * 128, STAGE = (BM + BN) * 128;
+  static_assert(S >= 2, "ring needs two stages");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int nwg = g.gm * g.gn;
+  const int per = g.gm * g.gn;
+  const int nwg = MODE == kDgradS2 ? 4 * per : per;
   int bid = blockIdx.x;
   {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  // parity class (kDgradS2): heaviest class (1,1) first so the long blocks start early
+  int cls = -1, py = 0, px = 0, kh0 = 0, kw0 = 0, ntx = 1, nk = g.Kpad >> 6;
+  if (MODE == kDgradS2) {
+    const int q = bid / per;
+    bid -= q * per;
+    cls = 3 - q; py = cls >> 1; px = cls & 1;
+    kh0 = (py + g.pad) & 1; kw0 = (px + g.pad) & 1;   // first tap of this parity, then every 2nd
+    const int nty = (g.KH - kh0 + 1) >> 1;
+    ntx = (g.KW - kw0 + 1) >> 1;
+    nk = (nty * ntx) << (g.log2SC - 6);
   }
   const int tm = bid / g.gn, tn = bid - tm * g.gn;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -388,6 +431,7 @@ __global__ __launch_bounds__(kThreads) void conv_lds3_kernel(const bf16* __restr
       const int y = rem / g.RW, x = rem - y * g.RW;
       a_pix[i] = n * g.SH * g.SW;
       if (MODE == kDgrad) { a_y[i] = y + g.pad; a_x[i] = x + g.pad; }
+      else if (MODE == kDgradS2) { a_y[i] = y; a_x[i] = x; }
       else { a_y[i] = y * g.stride - g.pad; a_x[i] = x * g.stride - g.pad; }
     }
   }
@@ -403,16 +447,23 @@ __global__ __launch_bounds__(kThreads) void conv_lds3_kernel(const bf16* __restr
     const int k0 = kt * 64;
     char* As = smem + buf * STAGE;
     char* Bs = As + SA;
-#pragma unroll
-    for (int j = 0; j < B_INS; ++j)
-      glds16(b_src[j] ? (const void*)(b_src[j] + k0) : (const void*)zp, Bs + (j * 32 + wave * 8) * 128);
-    int kh = 0, kw = 0, c0 = k0;
+    int kh = 0, kw = 0, c0 = k0, boff = k0;
     if (MODE != kGemm) {
       const int tap = k0 >> g.log2SC;
       c0 = k0 & (g.SC - 1);
-      kh = tap / g.KW;
-      kw = tap - kh * g.KW;
+      if (MODE == kDgradS2) {
+        const int th = ntx == 2 ? tap >> 1 : tap, tw = tap - th * ntx;
+        kh = kh0 + 2 * th;
+        kw = kw0 + 2 * tw;
+        boff = (kh * g.KW + kw) * g.SC + c0;
+      } else {
+        kh = tap / g.KW;
+        kw = tap - kh * g.KW;
+      }
     }
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j)
+      glds16(b_src[j] ? (const void*)(b_src[j] + boff) : (const void*)zp, Bs + (j * 32 + wave * 8) * 128);
 #pragma unroll
     for (int i = 0; i < A_INS; ++i) {
       const void* p = zp;
@@ -423,6 +474,10 @@ __global__ __launch_bounds__(kThreads) void conv_lds3_kernel(const bf16* __restr
         bool ok = a_ok[i];
         if (MODE == kFwd) {
           sy = a_y[i] + kh; sx = a_x[i] + kw;
+        } else if (MODE == kDgradS2) {
+          // dX(2yy+py) <- dY((2yy + py + pad - kh) / 2); the numerator is even by construction
+          sy = a_y[i] + ((py + g.pad - kh) >> 1);
+          sx = a_x[i] + ((px + g.pad - kw) >> 1);
         } else {
           const int ty = a_y[i] - kh, tx = a_x[i] - kw;
           ok = ok && ty >= 0 && tx >= 0;
@@ -468,53 +523,86 @@ __global__ __launch_bounds__(kThreads) void conv_lds3_kernel(const bf16* __restr
     }
   };
 
-  const int nk = g.Kpad / 64;
-  issue(0, 0);
-  if (nk > 1) issue(1, 1);
-  int cur = 0;
+  // prologue: stages 0 .. S-2 in flight; step kt refills the buffer step kt-1 read
+  for (int s = 0; s < S - 1 && s < nk; ++s) issue(s, s);
+  int cur = 0, wbuf = S - 1;
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) vmcnt_barrier<LOADS>();   // stage kt landed (kt+1 may still fly)
-    else vmcnt_barrier<0>();
-    if (kt + 2 < nk) issue(kt + 2, cur == 0 ? 2 : cur - 1);   // the buffer computed at kt-1
+    const int left = nk - 1 - kt;
+    wait_ahead<LOADS, S - 2>(left < S - 2 ? left : S - 2);   // stage kt landed, for every wave
+    if (kt + S - 1 < nk) issue(kt + S - 1, wbuf);
     compute(cur);
-    cur = cur == 2 ? 0 : cur + 1;
+    cur = cur == S - 1 ? 0 : cur + 1;
+    wbuf = wbuf == S - 1 ? 0 : wbuf + 1;
   }
   asm volatile("s_barrier" ::: "memory");   // every wave done reading the ring before the epilogue reuses it
-  conv_epilogue<bf16, BM, BN>(acc, smem, g, bias, res, out, stats, m0, n0);
+  conv_epilogue<bf16, BM, BN>(acc, smem, g, bias, res, out, stats, m0, n0, cls);
 }
 
-template <int BM, int BN, int MODE>
+// K-steps of the longest work item (kDgradS2: the class with the most taps)
+int fast_nk(int mode, const Geom& g) {
+  if (mode != kDgradS2) return g.Kpad / 64;
+  int best = 0;
+  for (int cls = 0; cls < 4; ++cls) {
+    const int kh0 = ((cls >> 1) + g.pad) & 1, kw0 = ((cls & 1) + g.pad) & 1;
+    const int t = ((g.KH - kh0 + 1) >> 1) * ((g.KW - kw0 + 1) >> 1);
+    best = t > best ? t : best;
+  }
+  return best * g.SC / 64;
+}
+
+int stage_bytes(int tile) {
+  static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
+  return (bm[tile] + bn[tile]) * 128;
+}
+
+template <int BM, int BN, int MODE, int S>
 int launch_fast(const Geom& g0, const void* src, const void* w, const float* bias, const void* res, void* out,
                 float* stats, hipStream_t s) {
   Geom g = g0;
   g.gm = p6::ceil_div(g.M, BM);
   g.gn = p6::ceil_div(g.Ncols, BN);
-  const int ring = 3 * (BM + BN) * 128;
+  const int nk = fast_nk(MODE, g);
+  const int ring = (nk < S ? (nk > 0 ? nk : 1) : S) * (BM + BN) * 128;
   const int epi = BM * (BN * 2 + 16);
   const int lds = ring > epi ? ring : epi;
-  conv_lds3_kernel<BM, BN, MODE><<<g.gm * g.gn, kThreads, lds, s>>>((const bf16*)src, (const bf16*)w, bias,
-                                                                     (const bf16*)res, (bf16*)out, stats, g);
+  const int grid = g.gm * g.gn * (MODE == kDgradS2 ? 4 : 1);
+  conv_lds_kernel<BM, BN, MODE, S><<<grid, kThreads, lds, s>>>((const bf16*)src, (const bf16*)w, bias,
+                                                                (const bf16*)res, (bf16*)out, stats, g);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
 
-template <int MODE>
-int launch_fast_mode(const Geom& g, int tile, const void* src, const void* w, const float* bias, const void* res,
-                     void* out, float* stats, hipStream_t s) {
-  switch (tile) {
-    case 0: return launch_fast<128, 128, MODE>(g, src, w, bias, res, out, stats, s);
-    case 1: return launch_fast<128, 64, MODE>(g, src, w, bias, res, out, stats, s);
-    case 2: return launch_fast<64, 128, MODE>(g, src, w, bias, res, out, stats, s);
-    default: return launch_fast<64, 64, MODE>(g, src, w, bias, res, out, stats, s);
+template <int BM, int BN, int MODE>
+int launch_fast_s(const Geom& g, int stages, const void* src, const void* w, const float* bias, const void* res,
+                  void* out, float* stats, hipStream_t s) {
+  switch (stages) {
+    case 2: return launch_fast<BM, BN, MODE, 2>(g, src, w, bias, res, out, stats, s);
+    case 3: return launch_fast<BM, BN, MODE, 3>(g, src, w, bias, res, out, stats, s);
+    case 4: return launch_fast<BM, BN, MODE, 4>(g, src, w, bias, res, out, stats, s);
+    default:
+      if constexpr ((BM + BN) * 128 * 6 <= 160 * 1024) return launch_fast<BM, BN, MODE, 6>(g, src, w, bias, res, out,
+                                                                                           stats, s);
+      else return launch_fast<BM, BN, MODE, 4>(g, src, w, bias, res, out, stats, s);
   }
 }
 
-int dispatch_fast(int mode, const Geom& g, int tile, const void* src, const void* w, const float* bias,
+template <int MODE>
+int launch_fast_mode(const Geom& g, int tile, int stages, const void* src, const void* w, const float* bias,
+                     const void* res, void* out, float* stats, hipStream_t s) {
+  switch (tile) {
+    case 0: return launch_fast_s<128, 128, MODE>(g, stages, src, w, bias, res, out, stats, s);
+    case 1: return launch_fast_s<128, 64, MODE>(g, stages, src, w, bias, res, out, stats, s);
+    default: return launch_fast_s<64, 64, MODE>(g, stages, src, w, bias, res, out, stats, s);
+  }
+}
+
+int dispatch_fast(int mode, const Geom& g, int tile, int stages, const void* src, const void* w, const float* bias,
                   const void* res, void* out, float* stats, hipStream_t s) {
   switch (mode) {
-    case kGemm: return launch_fast_mode<kGemm>(g, tile, src, w, bias, res, out, stats, s);
-    case kFwd: return launch_fast_mode<kFwd>(g, tile, src, w, bias, res, out, stats, s);
-    default: return launch_fast_mode<kDgrad>(g, tile, src, w, bias, res, out, stats, s);
+    case kGemm: return launch_fast_mode<kGemm>(g, tile, stages, src, w, bias, res, out, stats, s);
+    case kFwd: return launch_fast_mode<kFwd>(g, tile, stages, src, w, bias, res, out, stats, s);
+    case kDgradS2: return launch_fast_mode<kDgradS2>(g, tile, stages, src, w, bias, res, out, stats, s);
+    default: return launch_fast_mode<kDgrad>(g, tile, stages, src, w, bias, res, out, stats, s);
   }
 }
 
@@ -589,8 +677,8 @@ bool fast_ok(int dtype, int mode, const Geom& g) {
   return mode == kGemm || g.SC % 64 == 0;
 }
 
-int pick_tile_fast(int M, int N) {
-  auto blocks = [&](int bm, int bn) { return (int64_t)p6::ceil_div(M, bm) * p6::ceil_div(N, bn); };
+int pick_tile_fast(int64_t M, int N, int mult) {
+  auto blocks = [&](int bm, int bn) { return (int64_t)p6::ceil_div(M, (int64_t)bm) * p6::ceil_div(N, bn) * mult; };
   if (N <= 64) return blocks(128, 64) >= 256 ? 1 : 3;
   if (blocks(128, 128) >= 256) return 0;
   if (blocks(128, 64) >= 256) return 1;
@@ -602,20 +690,50 @@ int env_int(const char* name, int dflt) {
   return (v && *v) ? atoi(v) : dflt;
 }
 
-int choose(int dtype, int mode, const Geom& g, bool* fast) {
+struct Plan {
+  bool fast;
+  int mode, tile, stages;
+  Geom g;
+};
+
+// stride-2 data gradient as four parity classes: needs every dX pixel's class to
+// have the same extent (H, W even; Ho = H / 2, Wo = W / 2)
+bool s2_ok(const Geom& g) {
+  return g.stride == 2 && (g.RH & 1) == 0 && (g.RW & 1) == 0 && g.SH == g.RH / 2 && g.SW == g.RW / 2;
+}
+
+Plan choose(int dtype, int mode, const Geom& g) {
   const char* impl = getenv("POSE6D_CONV_IMPL");
-  *fast = fast_ok(dtype, mode, g) && !(impl && strcmp(impl, "base") == 0);
-  const int t = *fast ? pick_tile_fast(g.M, g.Ncols) : pick_tile(g.M, g.Ncols);
-  return env_int("POSE6D_CONV_TILE", t);
+  Plan p{};
+  p.fast = fast_ok(dtype, mode, g) && !(impl && strcmp(impl, "base") == 0);
+  p.mode = mode;
+  p.g = g;
+  if (!p.fast) {
+    p.tile = env_int("POSE6D_CONV_TILE", pick_tile(g.M, g.Ncols));
+    return p;
+  }
+  if (mode == kDgrad && s2_ok(g) && env_int("POSE6D_CONV_S2", 1)) {
+    p.mode = kDgradS2;
+    p.g.M = g.M / 4;
+    p.g.RH = g.RH / 2;
+    p.g.RW = g.RW / 2;
+  }
+  p.tile = env_int("POSE6D_CONV_TILE", pick_tile_fast(p.g.M, g.Ncols, p.mode == kDgradS2 ? 4 : 1));
+  if (p.tile == 2) p.tile = 3;   // no 64x128 instance on the fast path
+  p.stages = env_int("POSE6D_CONV_STAGES", 3);
+  if (p.stages < 2) p.stages = 2;
+  if (p.stages > 6) p.stages = 6;
+  if (p.stages == 5) p.stages = 4;
+  if (p.tile == 0 && p.stages > 4) p.stages = 4;   // 6 x 32 KiB exceeds the 160 KiB LDS
+  return p;
 }
 
 int run_conv(int dtype, int mode, const Geom& g, const void* src, const void* w, const float* bias, const void* res,
              void* out, float* stats, hipStream_t s) {
-  bool fast;
-  const int tile = choose(dtype, mode, g, &fast);
-  if (fast) return dispatch_fast(mode, g, tile, src, w, bias, res, out, stats, s);
-  return dtype == POSE6D_DT_BF16 ? dispatch<bf16>(mode, g, tile, src, w, bias, res, out, stats, s)
-                                 : dispatch<float>(mode, g, tile, src, w, bias, res, out, stats, s);
+  const Plan p = choose(dtype, mode, g);
+  if (p.fast) return dispatch_fast(p.mode, p.g, p.tile, p.stages, src, w, bias, res, out, stats, s);
+  return dtype == POSE6D_DT_BF16 ? dispatch<bf16>(mode, g, p.tile, src, w, bias, res, out, stats, s)
+                                 : dispatch<float>(mode, g, p.tile, src, w, bias, res, out, stats, s);
 }
 
 Geom fwd_geom(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad, int Ho, int Wo,
@@ -675,14 +793,14 @@ extern "C" int pose6d_conv2d_dgrad(int32_t dtype, const void* dy, const void* wt
 }
 
 // launch variant of a forward / data-gradient conv, for profiling joins:
-// (fast << 8) | (mode << 4) | tile, tile 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64
+// (stages << 12) | (fast << 8) | (mode << 4) | tile, tile 0 = 128x128, 1 = 128x64,
+// 2 = 64x128, 3 = 64x64 (stages 0 on the register-staged path)
 extern "C" int pose6d_conv_variant(int32_t dtype, int32_t pass, int32_t N, int32_t H, int32_t W, int32_t Cin,
                                    int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho,
                                    int32_t Wo) {
   int mode;
   const Geom g = pass == 0 ? fwd_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode)
                            : dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
-  bool fast;
-  const int tile = choose(dtype, mode, g, &fast);
-  return ((int)fast << 8) | (mode << 4) | tile;
+  const Plan p = choose(dtype, mode, g);
+  return (p.stages << 12) | ((int)p.fast << 8) | (p.mode << 4) | p.tile;
 }

@@ -18,7 +18,7 @@ def _sym(v, T):
     bm, bn = TILES[v & 15]
     mode = (v >> 4) & 15
     if (v >> 8) & 1:
-        return f"conv_lds3_kernel<{bm}, {bn}, {mode}>"
+        return f"conv_lds_kernel<{bm}, {bn}, {mode}, {v >> 12}>"
     return f"conv_igemm_kernel<{T}, {bm}, {bn}, {mode}>"
 
 

@@ -12,6 +12,7 @@ CONFIGS = [
     (2, 28, 28, 256, 512, 1, 2, 0, False),   # downsample 1x1/s2
     (2, 14, 14, 64, 64, 3, 1, 1, False),     # bottleneck 3x3
     (2, 28, 28, 128, 128, 3, 2, 1, False),   # stride-2 3x3
+    (2, 15, 15, 128, 64, 3, 2, 1, False),    # stride-2 3x3, odd extent (no parity-class split)
     (2, 32, 32, 3, 64, 7, 2, 3, False),      # stem 7x7/s2, Cin 3 padded to 4
     (2, 16, 16, 32, 64, 5, 1, 2, True),      # z-CNN 5x5 (+bias)
     (2, 32, 32, 3, 32, 7, 2, 3, True),       # z-CNN stem, Cout 32 (+bias)
@@ -100,6 +101,54 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
         db = torch.empty(Cout, device=dev)
         call("channel_sum", dt, dyd, N * Ho * Wo, Cout, db, 0, stream())
         _close(db, dy.sum((0, 2, 3)), tol, "bias grad")
+
+
+FAST_CONFIGS = [
+    (2, 14, 14, 64, 128, 1, 1, 0),    # GEMM mode
+    (2, 14, 14, 64, 64, 3, 1, 1),     # 3x3 implicit GEMM
+    (2, 28, 28, 128, 128, 3, 2, 1),   # 3x3/s2: parity-class dgrad
+    (2, 28, 28, 256, 512, 1, 2, 0),   # 1x1/s2: parity classes with zero taps
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", FAST_CONFIGS)
+def test_conv_fast_variants_bit_identical(cfg, monkeypatch):
+    """Every LDS-ring depth / tile of the bf16 fast path (and the parity-class
+    stride-2 dgrad vs the masked gather) accumulates each output in the same K
+    order, so all of them must agree bit for bit."""
+    from pose6d._lib import call, stream
+    from pose6d.trunk import DTYPES, pack_single
+    N, H, W, Cin, Cout, k, s, p = cfg
+    g = torch.Generator().manual_seed(7)
+    dev, dtype = "cuda", torch.bfloat16
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    x = torch.randn(N, H, W, Cin, generator=g).to(dev, dtype)
+    w = (torch.randn(Cout, Cin, k, k, generator=g) * 0.05).to(dev)
+    dy = torch.randn(N, Ho, Wo, Cout, generator=g).to(dev, dtype)
+    dres = torch.randn(N, H, W, Cin, generator=g).to(dev, dtype)
+    wp, wt = pack_single(w, Cin, dtype)
+    dt = DTYPES[dtype]
+
+    def run():
+        y = torch.empty(N, Ho, Wo, Cout, device=dev, dtype=dtype)
+        dx = torch.empty(N, H, W, Cin, device=dev, dtype=dtype)
+        call("conv2d_fwd", dt, x, wp, None, y, None, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream())
+        call("conv2d_dgrad", dt, dy, wt, dres, dx, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream())
+        torch.cuda.synchronize()
+        return y.cpu(), dx.cpu()
+
+    y0, dx0 = run()
+    variants = [{"POSE6D_CONV_STAGES": str(st), "POSE6D_CONV_TILE": str(t)} for st in (2, 3, 4, 6) for t in (0, 1, 3)]
+    variants.append({"POSE6D_CONV_S2": "0"})
+    for env in variants:
+        for key in ("POSE6D_CONV_STAGES", "POSE6D_CONV_TILE", "POSE6D_CONV_S2"):
+            monkeypatch.delenv(key, raising=False)
+        for key, v in env.items():
+            monkeypatch.setenv(key, v)
+        y1, dx1 = run()
+        assert torch.equal(y0, y1), f"fwd differs under {env}"
+        assert torch.equal(dx0, dx1), f"dgrad differs under {env}"
 
 
 @pytest.mark.gpu

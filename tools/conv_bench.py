@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--passes", default="fwd,dgrad,wgrad")
     ap.add_argument("--impls", default="base,fast")
     ap.add_argument("--tiles", default="auto,0,1,3")
+    ap.add_argument("--stages", default="auto", help="fast-path LDS ring depths to sweep, e.g. auto,2,3,4,6")
     ap.add_argument("--B", type=int, default=32)
     a = ap.parse_args()
     B, dt, dtype, dev = a.B, DTYPES[torch.bfloat16], torch.bfloat16, "cuda"
@@ -69,25 +70,28 @@ def main():
         for ps in a.passes.split(","):
             impls = a.impls.split(",") if ps != "wgrad" else ["base"]
             tiles = a.tiles.split(",") if ps != "wgrad" else ["auto"]
-            best = None
             for impl in impls:
+                stages = a.stages.split(",") if impl == "fast" else ["auto"]
                 for t in tiles:
-                    os.environ["POSE6D_CONV_IMPL"] = impl
-                    if t == "auto":
-                        os.environ.pop("POSE6D_CONV_TILE", None)
-                    else:
-                        os.environ["POSE6D_CONV_TILE"] = t
-                    try:
-                        sec = timeit(fns[ps])
-                    except Exception as e:  # noqa: BLE001
-                        line += f" {ps}:{impl}/{t}=ERR"
-                        continue
-                    tf = flops / sec / 1e12
-                    line += f" {ps[0]}{impl[0]}{t}:{sec * 1e6:6.1f}us/{tf:5.0f}T"
-                    if t == "auto":
-                        tot[(ps, impl)] = tot.get((ps, impl), 0.0) + sec
-        os.environ.pop("POSE6D_CONV_IMPL", None)
-        os.environ.pop("POSE6D_CONV_TILE", None)
+                    for st in stages:
+                        os.environ["POSE6D_CONV_IMPL"] = impl
+                        for key, val in (("POSE6D_CONV_TILE", t), ("POSE6D_CONV_STAGES", st)):
+                            if val == "auto":
+                                os.environ.pop(key, None)
+                            else:
+                                os.environ[key] = val
+                        try:
+                            sec = timeit(fns[ps])
+                        except Exception as e:  # noqa: BLE001
+                            line += f" {ps}:{impl}/{t}/{st}=ERR({str(e)[:120]})"
+                            continue
+                        tf = flops / sec / 1e12
+                        tag = f"{ps[0]}{impl[0]}{t}" + (f"s{st}" if impl == "fast" else "")
+                        line += f" {tag}:{sec * 1e6:6.1f}us/{tf:5.0f}T"
+                        if t == "auto" and st == "auto":
+                            tot[(ps, impl)] = tot.get((ps, impl), 0.0) + sec
+        for key in ("POSE6D_CONV_IMPL", "POSE6D_CONV_TILE", "POSE6D_CONV_STAGES"):
+            os.environ.pop(key, None)
         print(line, flush=True)
     print("totals (auto tile, one instance per distinct shape):",
           {f"{k[0]}/{k[1]}": round(v * 1e3, 3) for k, v in tot.items()})
