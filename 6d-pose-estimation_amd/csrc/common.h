@@ -47,6 +47,31 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// counter-based uniform in [0,1): splitmix64 finaliser of (seed, index); the
+// dropout masks of every kernel draw from it (mask = uniform >= p)
+__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+// sum over a workgroup of NT threads (NT / 64 waves); `red` holds NT / 64 floats.
+// Every thread gets the total.  Contains barriers: call from uniform control flow.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) t += red[w];
+  return t;
+}
+
 inline hipStream_t stream_of(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }

@@ -21,6 +21,7 @@
 #include <string.h>
 
 #include "common.h"
+#include "lds_dma.h"
 
 namespace {
 
@@ -349,30 +350,35 @@ __global__ __launch_bounds__(kThreads) void conv_igemm_kernel(const T* __restric
 // S is picked per layer: deep rings for small, long-K grids (latency bound: one
 // workgroup per CU, each K-step short), shallow ones for big grids (occupancy).
 // ============================================================================
-__device__ uint4 g_zero_page[4];   // 64 zero bytes (static storage: zero-initialised)
-
-__device__ __forceinline__ int swz8(int row) { return (row >> 1) & 7; }
-
-__device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
-                                   (void __attribute__((address_space(3)))*)lds_wave_base, 16, 0, 0);
-}
-
-template <int N>
-__device__ __forceinline__ void vmcnt_barrier() {
-  static_assert(N >= 0 && N < 64, "vmcnt is a 6-bit count");
-  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
-}
-
-// wait until at most `ahead` stages (LOADS DMA instructions each) are still in
-// flight, then barrier; `ahead` is wave-uniform, J the largest value it takes
-template <int LOADS, int J>
-__device__ __forceinline__ void wait_ahead(int ahead) {
-  if constexpr (J <= 0) {
-    vmcnt_barrier<0>();
+// Fragment reads of one k-half as ONE asm block: NR ds_read_b128 then
+// lgkmcnt(0).  Written as plain C++ loads, hipcc cannot tell the ring slot being
+// read from the slots the in-flight LDS-DMA is filling and emits vmcnt(0) before
+// the first ds_read of every K-step, draining the whole prefetch ring (the .s
+// showed it: deeper rings bought nothing).  The counted vmcnt + barrier in the
+// K-loop is what orders these reads after the DMA that filled the slot.
+template <int NR>
+__device__ __forceinline__ void lds_read_frags(u32x4 (&f)[NR], const unsigned (&addr)[NR]) {
+  static_assert(NR == 4 || NR == 6 || NR == 8, "fragment batch of 4, 6 or 8 reads");
+  if constexpr (NR == 4) {
+    asm volatile(
+        "ds_read_b128 %0, %4\n\tds_read_b128 %1, %5\n\tds_read_b128 %2, %6\n\tds_read_b128 %3, %7\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3])
+        : "v"(addr[0]), "v"(addr[1]), "v"(addr[2]), "v"(addr[3]));
+  } else if constexpr (NR == 6) {
+    asm volatile(
+        "ds_read_b128 %0, %6\n\tds_read_b128 %1, %7\n\tds_read_b128 %2, %8\n\tds_read_b128 %3, %9\n\t"
+        "ds_read_b128 %4, %10\n\tds_read_b128 %5, %11\n\ts_waitcnt lgkmcnt(0)"
+        : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]), "=&v"(f[4]), "=&v"(f[5])
+        : "v"(addr[0]), "v"(addr[1]), "v"(addr[2]), "v"(addr[3]), "v"(addr[4]), "v"(addr[5]));
   } else {
-    if (ahead >= J) vmcnt_barrier<J * LOADS>();
-    else wait_ahead<LOADS, J - 1>(ahead);
+    asm volatile(
+        "ds_read_b128 %0, %8\n\tds_read_b128 %1, %9\n\tds_read_b128 %2, %10\n\tds_read_b128 %3, %11\n\t"
+        "ds_read_b128 %4, %12\n\tds_read_b128 %5, %13\n\tds_read_b128 %6, %14\n\tds_read_b128 %7, %15\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]), "=&v"(f[4]), "=&v"(f[5]), "=&v"(f[6]), "=&v"(f[7])
+        : "v"(addr[0]), "v"(addr[1]), "v"(addr[2]), "v"(addr[3]), "v"(addr[4]), "v"(addr[5]), "v"(addr[6]),
+          "v"(addr[7]));
   }
 }
 
@@ -395,12 +401,14 @@ __global__ __launch_bounds__(kThreads) void conv_lds_kernel(const bf16* __restri
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-  // parity class (kDgradS2): heaviest class (1,1) first so the long blocks start early
+  // parity class (kDgradS2): the four classes of one tile are consecutive logical
+  // ids, so every XCD gets an even share of the heavy and the empty classes and the
+  // four blocks that gather the same dY rows run on the same L2
   int cls = -1, py = 0, px = 0, kh0 = 0, kw0 = 0, ntx = 1, nk = g.Kpad >> 6;
   if (MODE == kDgradS2) {
-    const int q = bid / per;
-    bid -= q * per;
-    cls = 3 - q; py = cls >> 1; px = cls & 1;
+    cls = 3 - (bid & 3);
+    bid >>= 2;
+    py = cls >> 1; px = cls & 1;
     kh0 = (py + g.pad) & 1; kw0 = (px + g.pad) & 1;   // first tap of this parity, then every 2nd
     const int nty = (g.KH - kh0 + 1) >> 1;
     ntx = (g.KW - kw0 + 1) >> 1;
@@ -497,29 +505,39 @@ __global__ __launch_bounds__(kThreads) void conv_lds_kernel(const bf16* __restri
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // per-lane fragment byte offsets inside a ring slot (row-dependent swizzle), per k-half
   const int fr = lane & 15, fc = lane >> 4;
+  unsigned frag_off[2][TM + TN];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wm * (BM / 2) + i * 16 + fr;
+      frag_off[kk][i] = row * 128 + (((fc + 4 * kk) ^ swz8(row)) << 4);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int row = wn * (BN / 2) + j * 16 + fr;
+      frag_off[kk][TM + j] = SA + row * 128 + (((fc + 4 * kk) ^ swz8(row)) << 4);
+    }
+  }
+  const unsigned ring_base = lds_addr(smem);
   auto compute = [&](int buf) {
-    const char* As = smem + buf * STAGE;
-    const char* Bs = As + SA;
+    const unsigned slot = ring_base + buf * STAGE;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      uint4 af[TM], bfr[TN];
+      unsigned addr[TM + TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * (BM / 2) + i * 16 + fr;
-        af[i] = *reinterpret_cast<const uint4*>(As + row * 128 + (((fc + 4 * kk) ^ swz8(row)) << 4));
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wn * (BN / 2) + j * 16 + fr;
-        bfr[j] = *reinterpret_cast<const uint4*>(Bs + row * 128 + (((fc + 4 * kk) ^ swz8(row)) << 4));
-      }
+      for (int r = 0; r < TM + TN; ++r) addr[r] = slot + frag_off[kk][r];
+      u32x4 f[TM + TN];
+      lds_read_frags<TM + TN>(f, addr);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
-                                                              __builtin_bit_cast(bf16x8, bfr[j]), acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f[i]),
+                                                              __builtin_bit_cast(bf16x8, f[TM + j]), acc[i][j], 0, 0,
+                                                              0);
     }
   };
 
@@ -677,11 +695,11 @@ bool fast_ok(int dtype, int mode, const Geom& g) {
   return mode == kGemm || g.SC % 64 == 0;
 }
 
+// 64x64 tiles: measured best or within a few % on every ResNet50 layer at batch
+// 32 (tools/conv_bench.py sweep) -- occupancy beats per-wave operand reuse at
+// these grid sizes
 int pick_tile_fast(int64_t M, int N, int mult) {
-  auto blocks = [&](int bm, int bn) { return (int64_t)p6::ceil_div(M, (int64_t)bm) * p6::ceil_div(N, bn) * mult; };
-  if (N <= 64) return blocks(128, 64) >= 256 ? 1 : 3;
-  if (blocks(128, 128) >= 256) return 0;
-  if (blocks(128, 64) >= 256) return 1;
+  (void)M; (void)N; (void)mult;
   return 3;
 }
 
@@ -720,7 +738,12 @@ Plan choose(int dtype, int mode, const Geom& g) {
   }
   p.tile = env_int("POSE6D_CONV_TILE", pick_tile_fast(p.g.M, g.Ncols, p.mode == kDgradS2 ? 4 : 1));
   if (p.tile == 2) p.tile = 3;   // no 64x128 instance on the fast path
-  p.stages = env_int("POSE6D_CONV_STAGES", 3);
+  // two slots (32 KiB at 64x64) keep several workgroups per CU resident, which hides
+  // the DMA latency better than a deeper ring; only long-K grids that leave CUs
+  // idle (one wave of workgroups) take a 4-deep ring
+  const int64_t grid = (int64_t)p6::ceil_div(p.g.M, p.tile <= 1 ? 128 : 64) *
+                       p6::ceil_div(g.Ncols, p.tile == 0 ? 128 : 64) * (p.mode == kDgradS2 ? 4 : 1);
+  p.stages = env_int("POSE6D_CONV_STAGES", (fast_nk(p.mode, p.g) > 24 && grid <= 512) ? 4 : 2);
   if (p.stages < 2) p.stages = 2;
   if (p.stages > 6) p.stages = 6;
   if (p.stages == 5) p.stages = 4;

@@ -87,23 +87,17 @@ __global__ void gemm_splitk_reduce_kernel(const float* __restrict__ part, int sp
   C[m * ldc + n] = v;
 }
 
-// db[n] (+)= sum_m dy[m][n]
-__global__ void colsum_kernel(const float* __restrict__ dy, float* __restrict__ db, int M, int N, int accumulate) {
+// db[n] (+)= sum_m dy[m * ldy + n]
+__global__ void colsum_kernel(const float* __restrict__ dy, int64_t ldy, float* __restrict__ db, int M, int N,
+                              int accumulate) {
   const int n = blockIdx.x * kThreads + threadIdx.x;
   if (n >= N) return;
   float s = 0.f;
-  for (int m = 0; m < M; ++m) s += dy[(int64_t)m * N + n];
+  for (int m = 0; m < M; ++m) s += dy[m * ldy + n];
   db[n] = accumulate ? db[n] + s : s;
 }
 
-// counter-based uniform in [0,1): hash of (seed, index)
-__device__ __forceinline__ float uniform(uint64_t seed, uint64_t i) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (float)(z >> 40) * (1.0f / 16777216.0f);
-}
+using p6::uniform01;
 
 // BatchNorm1d over the batch (one thread per column) + optional ReLU + Dropout.
 __global__ void bn1d_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int M, int C,
@@ -137,7 +131,7 @@ __global__ void bn1d_fwd_kernel(const float* __restrict__ x, float* __restrict__
     float v = (x[o] - mean) * inv * g + b;
     if (relu) v = fmaxf(v, 0.f);
     if (p_drop > 0.f) {
-      const bool keep = uniform(seedp[0] ^ salt, (uint64_t)o) >= p_drop;
+      const bool keep = uniform01(seedp[0] ^ salt, (uint64_t)o) >= p_drop;
       mask[o] = keep;
       v = keep ? v * keep_scale : 0.f;
     }
@@ -186,7 +180,7 @@ __global__ void act_fwd_kernel(const float* __restrict__ x, float* __restrict__ 
   if (act == 1) v = fmaxf(v, 0.f);
   else if (act == 2) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));  // exact GELU
   if (p_drop > 0.f) {
-    const bool keep = uniform(seedp[0] ^ salt, (uint64_t)i) >= p_drop;
+    const bool keep = uniform01(seedp[0] ^ salt, (uint64_t)i) >= p_drop;
     mask[i] = keep;
     v = keep ? v / (1.0f - p_drop) : 0.f;
   }
@@ -242,9 +236,11 @@ extern "C" int pose6d_gemm_f32(const float* A, int64_t sam, int64_t sak, const f
   return POSE6D_OK;
 }
 
-extern "C" int pose6d_colsum_f32(const float* dy, float* db, int32_t M, int32_t N, int32_t accumulate, void* stream) {
+extern "C" int pose6d_colsum_f32(const float* dy, int64_t ldy, float* db, int32_t M, int32_t N, int32_t accumulate,
+                                 void* stream) {
+  P6_CHECK_ARG(M >= 0 && N >= 0 && ldy >= N, "pose6d_colsum_f32: bad shape");
   if (N == 0) return POSE6D_OK;
-  colsum_kernel<<<p6::ceil_div(N, kThreads), kThreads, 0, p6::stream_of(stream)>>>(dy, db, M, N, accumulate);
+  colsum_kernel<<<p6::ceil_div(N, kThreads), kThreads, 0, p6::stream_of(stream)>>>(dy, ldy, db, M, N, accumulate);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }

@@ -1,11 +1,13 @@
 """Fully-connected head engine: executes an nn.Sequential of Linear / BatchNorm1d /
-ReLU / GELU / Dropout (/ LayerNorm, see layernorm ops) forward and backward on the
-pose6d HIP kernels (fp32).
+LayerNorm / ReLU / GELU / Dropout forward and backward on the pose6d HIP kernels
+(fp32).
 
 Replaces the rot/trans/z heads of the reference (pose_net_rgb.py:23-50,
-pose_net_rgb_geometric.py:23-33,58-65, pose_net_rgbd_geometric.py:28-38).
+pose_net_rgb_geometric.py:23-33,58-65, pose_net_rgbd_geometric.py:28-38) and the
+fusion MLP / heads of PoseNetRGBD (pose_net_rgbd.py:80-105).
 Linear -> BatchNorm1d -> ReLU -> Dropout runs as 2 launches (GEMM + fused
-BN/ReLU/dropout column kernel); buffers are preallocated per batch size.
+BN/ReLU/dropout column kernel), Linear -> LayerNorm -> GELU -> Dropout as 2
+(GEMM + fused row kernel); buffers are preallocated per batch size.
 """
 import torch
 import torch.nn as nn
@@ -39,6 +41,19 @@ class HeadEngine:
                 i += 1
                 if i < len(mods) and isinstance(mods[i], nn.ReLU):
                     st.act = 1
+                    i += 1
+                if i < len(mods) and isinstance(mods[i], nn.Dropout):
+                    st.drop = mods[i]
+                    i += 1
+            elif isinstance(m, nn.LayerNorm):
+                if len(m.normalized_shape) != 1 or not m.elementwise_affine or m.bias is None:
+                    raise Pose6dError("HeadEngine: LayerNorm must be affine over the last dimension")
+                st.kind, st.mod, st.act, st.drop = "ln", m, 0, None
+                i += 1
+                if i < len(mods) and isinstance(mods[i], (nn.ReLU, nn.GELU)):
+                    if isinstance(mods[i], nn.GELU) and getattr(mods[i], "approximate", "none") != "none":
+                        raise Pose6dError("only exact (erf) GELU is implemented")
+                    st.act = 1 if isinstance(mods[i], nn.ReLU) else 2
                     i += 1
                 if i < len(mods) and isinstance(mods[i], nn.Dropout):
                     st.drop = mods[i]
@@ -78,8 +93,13 @@ class HeadEngine:
             st.y = torch.empty(B, d, device=device, dtype=torch.float32)
             st.dx = torch.empty(B, (st.mod.in_features if st.kind == "linear" else d), device=device,
                                 dtype=torch.float32)
-            if st.kind in ("bn1d", "act"):
+            if st.kind in ("bn1d", "act", "ln"):
                 st.mask = torch.empty(B, d, device=device, dtype=torch.uint8)
+            if st.kind == "ln":
+                if st.mod.normalized_shape[0] != d:
+                    raise Pose6dError("HeadEngine: LayerNorm width mismatch")
+                st.smean = torch.empty(B, device=device, dtype=torch.float32)
+                st.srstd = torch.empty(B, device=device, dtype=torch.float32)
             if st.kind == "bn1d":
                 st.smean = torch.empty(d, device=device, dtype=torch.float32)
                 st.sinv = torch.empty(d, device=device, dtype=torch.float32)
@@ -116,6 +136,11 @@ class HeadEngine:
                          bn.running_var, bn.num_batches_tracked, float(bn.momentum if bn.momentum is not None else 0.1),
                          float(bn.eps), int(bn.training), st.act, p, seed_dev, (salt * 131 + i) & 0xFFFFFFFFFFFF,
                          st.mask, st.smean, st.sinv, st_)
+                elif st.kind == "ln":
+                    ln = st.mod
+                    call("layernorm_fwd", cur, st.dim, st.y, st.dim, None, B, st.dim, ln.weight.detach(),
+                         ln.bias.detach(), float(ln.eps), st.act, p, seed_dev, (salt * 131 + i) & 0xFFFFFFFFFFFF,
+                         st.mask, st.smean, st.srstd, st_)
                 else:
                     call("act_fwd", cur, st.y, B * st.dim, st.act, p, seed_dev, (salt * 131 + i) & 0xFFFFFFFFFFFF,
                          st.mask, st_)
@@ -143,7 +168,7 @@ class HeadEngine:
                 call("gemm_f32", g, 1, N, st.x, K, 1, grad_of(m.weight), K, None, N, K, B, 1.0, float(acc),
                      self.ws, self.ws.numel(), st_)
                 if m.bias is not None:
-                    call("colsum_f32", g, grad_of(m.bias), B, N, acc, st_)
+                    call("colsum_f32", g, N, grad_of(m.bias), B, N, acc, st_)
                 if last and not need_dx:
                     return None
                 call("gemm_f32", g, N, 1, m.weight.detach(), K, 1, st.dx, K, None, B, K, N, 1.0, 0.0, self.ws,
@@ -153,6 +178,11 @@ class HeadEngine:
                 call("bn1d_bwd", g, st.x, st.y, B, st.dim, bn.weight.detach(), st.smean, st.sinv,
                      int(st.bn_train), st.act, st.p, st.mask, st.dx, grad_of(bn.weight), grad_of(bn.bias), acc,
                      st_)
+            elif st.kind == "ln":
+                ln = st.mod
+                call("layernorm_bwd", g, st.dim, None, 0, st.x, st.dim, B, st.dim, ln.weight.detach(),
+                     ln.bias.detach(), st.smean, st.srstd, st.act, st.p, st.mask, st.dx, st.dim, 0,
+                     grad_of(ln.weight), grad_of(ln.bias), acc, st_)
             else:
                 call("act_bwd", g, st.x, st.dx, B * st.dim, st.act, st.p, st.mask, st_)
             g = st.dx
@@ -163,6 +193,6 @@ class HeadEngine:
         for st in reversed(self.stages):
             if st.kind == "linear":
                 out += [st.mod.weight] + ([st.mod.bias] if st.mod.bias is not None else [])
-            elif st.kind == "bn1d":
+            elif st.kind in ("bn1d", "ln"):
                 out += [st.mod.weight, st.mod.bias]
         return out

@@ -46,8 +46,11 @@ def conv_launches(eng):
                 call("conv2d_dgrad", dt, op.out.g, op.wt, None, op.dres, B, op.H, op.W, op.cin_pad, op.cout, op.k,
                      op.k, op.stride, op.pad, op.Ho, op.Wo, st)
             out.append((sym, flops, dgrad, op.name + ".dgrad"))
-        v = query("wgrad_variant", dt, M, op.cout, op.k * op.k * op.cin_pad)
-        sym = f"conv_wgrad_kernel<{T}, {128 if v & 2 else 64}, {128 if v & 1 else 64}>"
+        v = query("wgrad_variant", dt, M, op.cout, op.k * op.k * op.cin_pad, op.cin_pad)
+        if (v >> 8) & 1:
+            sym = f"conv_wgrad_lds_kernel<64, 64, {v >> 12}>"
+        else:
+            sym = f"conv_wgrad_kernel<{T}, {128 if v & 2 else 64}, {128 if v & 1 else 64}>"
         dw = torch.empty_like(op.conv.weight)
 
         def wgrad(op=op, dw=dw):

@@ -124,12 +124,15 @@ int pose6d_conv2d_fwd(int32_t dtype, const void *x, const void *wp, const float 
                       int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW,
                       int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, void *stream);
 /* kernel variant a conv launch selects (profiling joins): fwd/dgrad (pass 0/1):
- * (fast << 8) | (mode << 4) | tile (tile 0..3 = 128x128, 128x64, 64x128, 64x64;
- * mode 0 gemm, 1 im2col, 2 narrow stem, 3 dgrad; fast = LDS-DMA bf16 kernel);
- * wgrad: (BM == 128) << 1 | (BN == 128). */
+ * (stages << 12) | (fast << 8) | (mode << 4) | tile (tile 0..3 = 128x128, 128x64,
+ * 64x128, 64x64; mode 0 gemm, 1 im2col, 2 narrow stem, 3 dgrad, 4 stride-2 dgrad
+ * split into output parity classes; fast = LDS-DMA bf16 kernel with an LDS ring
+ * of `stages` K-steps, 0 on the register-staged kernel);
+ * wgrad (pose6d_wgrad_variant, Cin = the padded channel count): (stages << 12) |
+ * (fast << 8) | (BM == 128) << 1 | (BN == 128); fast = LDS-DMA 64x64 kernel. */
 int pose6d_conv_variant(int32_t dtype, int32_t pass, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout,
                         int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo);
-int pose6d_wgrad_variant(int32_t dtype, int32_t M, int32_t Cout, int32_t K);
+int pose6d_wgrad_variant(int32_t dtype, int32_t M, int32_t Cout, int32_t K, int32_t Cin);
 /* data gradient: dx [N][H][W][Cin] = conv_transpose(dy [N][Ho][Wo][Cout], wt) (+ dres if non-NULL) */
 int pose6d_conv2d_dgrad(int32_t dtype, const void *dy, const void *wt, const void *dres, void *dx, int32_t N,
                         int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
@@ -189,7 +192,9 @@ int pose6d_avgpool_bwd(int32_t dtype, const float *dy, void *dx, int32_t N, int3
 int pose6d_gemm_f32(const float *A, int64_t sam, int64_t sak, const float *B, int64_t sbk, int64_t sbn, float *C,
                     int64_t ldc, const float *bias, int32_t M, int32_t N, int32_t K, float alpha, float beta,
                     float *workspace, int64_t ws_floats, void *stream);
-int pose6d_colsum_f32(const float *dy, float *db, int32_t M, int32_t N, int32_t accumulate, void *stream);
+/* db[n] (+)= sum_m dy[m * ldy + n]  (Linear bias gradient; ldy >= N) */
+int pose6d_colsum_f32(const float *dy, int64_t ldy, float *db, int32_t M, int32_t N, int32_t accumulate,
+                      void *stream);
 /* BatchNorm1d (+ReLU) (+Dropout p_drop with a counter-based RNG keyed by the
  * device word *seed xor salt -- a device word so graph replays draw new masks) */
 int pose6d_bn1d_fwd(const float *x, float *y, int32_t M, int32_t C, const float *gamma, const float *beta,
@@ -204,6 +209,41 @@ int pose6d_act_fwd(const float *x, float *y, int64_t n, int32_t act, float p_dro
                    uint64_t salt, uint8_t *mask, void *stream);
 int pose6d_act_bwd(const float *dy, const float *x, float *dx, int64_t n, int32_t act, float p_drop,
                    const uint8_t *mask, void *stream);
+
+/* ------------------------------------------------------------------------
+ * RGB-D fusion (PoseNetRGBD, pose_net_rgbd.py:66-103,118-142), fp32.
+ * LayerNorm over rows of D (nn.LayerNorm(D): biased variance, eps), fused with
+ * act (0 none, 1 ReLU, 2 exact GELU) and Dropout(p) — the nn.Sequential runs
+ * LayerNorm -> GELU -> Dropout of `fusion` / `rot_head` / `trans_head`
+ * (pose_net_rgbd.py:72-103) and rgb_norm / depth_norm (:68-69, :127-128, act 0).
+ * Row strides (ld*) let the two normalised features land side by side in the
+ * (B, 2D) concatenation (:134) without a copy; y2 (optional, contiguous)
+ * receives a second copy.  mean / rstd (B each) are saved for the backward.
+ * Backward: dy (+ dy2 when non-null: a second gradient flowing into the same
+ * output, e.g. the residual and the concatenation branch) -> dx (+= when
+ * accumulate_dx), dgamma / dbeta (+= when accumulate).
+ * ---------------------------------------------------------------------- */
+int pose6d_layernorm_fwd(const float *x, int64_t ldx, float *y, int64_t ldy, float *y2, int32_t B, int32_t D,
+                         const float *gamma, const float *beta, float eps, int32_t act, float p_drop,
+                         const uint64_t *seed, uint64_t salt, uint8_t *mask, float *mean, float *rstd,
+                         void *stream);
+int pose6d_layernorm_bwd(const float *dy, int64_t lddy, const float *dy2, int64_t lddy2, const float *x,
+                         int64_t ldx, int32_t B, int32_t D, const float *gamma, const float *beta,
+                         const float *mean, const float *rstd, int32_t act, float p_drop, const uint8_t *mask,
+                         float *dx, int64_t lddx, int32_t accumulate_dx, float *dgamma, float *dbeta,
+                         int32_t accumulate, void *stream);
+
+/* CrossModalAttention core (pose_net_rgbd.py:23-35): per sample b,
+ *   attn = softmax((q_b k_b^T) * scale), q_b, k_b, v_b = (H, hd) views of rows
+ *   of the projections; out_b = dropout(attn) v_b, flattened back to H*hd.
+ * probs (B*H*H) keeps the pre-dropout softmax for the backward; mask (B*H*H)
+ * the dropout draw.  H <= 16. */
+int pose6d_xattn_fwd(const float *q, const float *k, const float *v, float *out, int32_t B, int32_t H, int32_t hd,
+                     float scale, float p_drop, const uint64_t *seed, uint64_t salt, float *probs, uint8_t *mask,
+                     void *stream);
+int pose6d_xattn_bwd(const float *dout, const float *q, const float *k, const float *v, const float *probs,
+                     const uint8_t *mask, int32_t B, int32_t H, int32_t hd, float scale, float p_drop, float *dq,
+                     float *dk, float *dv, void *stream);
 
 /* ------------------------------------------------------------------------
  * Optimiser — clip_grad_norm_(params, max_norm) + AdamW.step() of the callers

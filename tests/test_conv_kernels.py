@@ -130,25 +130,39 @@ def test_conv_fast_variants_bit_identical(cfg, monkeypatch):
     wp, wt = pack_single(w, Cin, dtype)
     dt = DTYPES[dtype]
 
+    from pose6d._lib import query
+    ws = torch.empty(query("conv2d_wgrad_workspace", dt, N, Ho, Wo, Cin, Cout, k, k) // 4 + 1, device=dev)
+
     def run():
         y = torch.empty(N, Ho, Wo, Cout, device=dev, dtype=dtype)
         dx = torch.empty(N, H, W, Cin, device=dev, dtype=dtype)
+        dw = torch.empty(Cout, Cin, k, k, device=dev)
         call("conv2d_fwd", dt, x, wp, None, y, None, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream())
         call("conv2d_dgrad", dt, dy, wt, dres, dx, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream())
+        call("conv2d_wgrad", dt, x, dy, dw, 0, ws, N, H, W, Cin, Cin, Cout, k, k, s, p, Ho, Wo, stream())
         torch.cuda.synchronize()
-        return y.cpu(), dx.cpu()
+        return y.cpu(), dx.cpu(), dw.cpu()
 
-    y0, dx0 = run()
+    y0, dx0, dw0 = run()
     variants = [{"POSE6D_CONV_STAGES": str(st), "POSE6D_CONV_TILE": str(t)} for st in (2, 3, 4, 6) for t in (0, 1, 3)]
     variants.append({"POSE6D_CONV_S2": "0"})
+    variants += [{"POSE6D_WGRAD_STAGES": str(st)} for st in (2, 3, 4)]
+    keys = ("POSE6D_CONV_STAGES", "POSE6D_CONV_TILE", "POSE6D_CONV_S2", "POSE6D_WGRAD_STAGES")
     for env in variants:
-        for key in ("POSE6D_CONV_STAGES", "POSE6D_CONV_TILE", "POSE6D_CONV_S2"):
+        for key in keys:
             monkeypatch.delenv(key, raising=False)
         for key, v in env.items():
             monkeypatch.setenv(key, v)
-        y1, dx1 = run()
+        y1, dx1, dw1 = run()
         assert torch.equal(y0, y1), f"fwd differs under {env}"
         assert torch.equal(dx0, dx1), f"dgrad differs under {env}"
+        assert torch.equal(dw0, dw1), f"wgrad differs under {env}"
+    # the register-staged weight gradient sums the pixels in other splits: close, not equal
+    for key in keys:
+        monkeypatch.delenv(key, raising=False)
+    monkeypatch.setenv("POSE6D_WGRAD_IMPL", "base")
+    _, _, dwb = run()
+    _close(dwb, dw0, 1e-5, "wgrad base vs LDS-DMA")
 
 
 @pytest.mark.gpu

@@ -14,15 +14,17 @@ EXPECTED = {
     "PoseNetRGB": (37162567, 354),
     "PoseNetRGBGeometric": (26603333, 368),
     "PoseNetRGBDGeometric": (26136132, 334),
+    "PoseNetRGBD": (70368519, 672),
 }
 
 
 def _models():
     from models.pose_net_rgb import PoseNetRGB
     from models.pose_net_rgb_geometric import PoseNetRGBGeometric
+    from models.pose_net_rgbd import PoseNetRGBD
     from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
     return {"PoseNetRGB": PoseNetRGB, "PoseNetRGBGeometric": PoseNetRGBGeometric,
-            "PoseNetRGBDGeometric": PoseNetRGBDGeometric}
+            "PoseNetRGBDGeometric": PoseNetRGBDGeometric, "PoseNetRGBD": PoseNetRGBD}
 
 
 @pytest.mark.parametrize("name", list(EXPECTED))
@@ -47,6 +49,8 @@ def _oracle_forward(name, P, inputs, training):
         return OR.forward_rgb(P, inputs["rgb"], training)
     if name == "PoseNetRGBGeometric":
         return OR.forward_rgb_geometric(P, inputs["rgb"], inputs["bbox"], inputs["K"], training)
+    if name == "PoseNetRGBD":
+        return OR.forward_rgbd(P, inputs["rgb"], inputs["depth"], training=training)
     return OR.forward_rgbd_geometric(P, inputs["rgb"], inputs["depth"], inputs["depth_raw"], inputs["bbox"],
                                      inputs["K"], training)
 
@@ -56,6 +60,8 @@ def _model_forward(name, m, inp):
         return m(inp["rgb"])
     if name == "PoseNetRGBGeometric":
         return m(inp["rgb"], inp["bbox"], inp["K"])
+    if name == "PoseNetRGBD":
+        return m(inp["rgb"], inp["depth"])
     return m(inp["rgb"], inp["depth"], inp["depth_raw"], inp["bbox"], inp["K"])
 
 

@@ -73,9 +73,9 @@ def main():
             for impl in impls:
                 stages = a.stages.split(",") if impl == "fast" else ["auto"]
                 for t in tiles:
-                    for st in stages:
+                    for nst in stages:
                         os.environ["POSE6D_CONV_IMPL"] = impl
-                        for key, val in (("POSE6D_CONV_TILE", t), ("POSE6D_CONV_STAGES", st)):
+                        for key, val in (("POSE6D_CONV_TILE", t), ("POSE6D_CONV_STAGES", nst)):
                             if val == "auto":
                                 os.environ.pop(key, None)
                             else:
@@ -83,12 +83,12 @@ def main():
                         try:
                             sec = timeit(fns[ps])
                         except Exception as e:  # noqa: BLE001
-                            line += f" {ps}:{impl}/{t}/{st}=ERR({str(e)[:120]})"
+                            line += f" {ps}:{impl}/{t}/{nst}=ERR({str(e)[:120]})"
                             continue
                         tf = flops / sec / 1e12
-                        tag = f"{ps[0]}{impl[0]}{t}" + (f"s{st}" if impl == "fast" else "")
+                        tag = f"{ps[0]}{impl[0]}{t}" + (f"s{nst}" if impl == "fast" else "")
                         line += f" {tag}:{sec * 1e6:6.1f}us/{tf:5.0f}T"
-                        if t == "auto" and st == "auto":
+                        if t == "auto" and nst == "auto":
                             tot[(ps, impl)] = tot.get((ps, impl), 0.0) + sec
         for key in ("POSE6D_CONV_IMPL", "POSE6D_CONV_TILE", "POSE6D_CONV_STAGES"):
             os.environ.pop(key, None)
