@@ -185,7 +185,7 @@ __global__ __launch_bounds__(kThreads) void bn_act_kernel(const T* __restrict__ 
 // ---------------------------------------------------------------- backward
 // grid (channel-chunk groups, row blocks): block = CL chunk-lanes (consecutive 16-B
 // chunks of a row: coalesced) x RL row-lanes; partial row = blockIdx.y.
-template <typename T>
+template <typename T, bool HAS_OUT>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce2_kernel(const T* __restrict__ dout, const T* __restrict__ out,
                                                                   const T* __restrict__ y,
                                                                   const float* __restrict__ mean,
@@ -204,11 +204,42 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce2_kernel(const T* __res
   for (int e = 0; e < E; ++e) { s[e] = q[e] = 0.f; mu[e] = mean[c0 + e]; iv[e] = inv[c0 + e]; }
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
   const int64_t r1 = min(M, r0 + rows_per_block);
-  for (int64_t r = r0 + rl; r < r1; r += RL) {
+  // U rows per trip with every load issued before any use: 3 * U 16-byte loads in
+  // flight per lane (one row per trip left this kernel latency bound at ~25 % of HBM)
+  constexpr int U = 4;
+  int64_t r = r0 + rl;
+  for (; r + (U - 1) * RL < r1; r += U * RL) {
+    uint4 dv[U], ov[U], yv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t off = (r + u * RL) * C + c0;
+      dv[u] = *reinterpret_cast<const uint4*>(dout + off);
+      if constexpr (HAS_OUT) ov[u] = *reinterpret_cast<const uint4*>(out + off);
+      yv[u] = *reinterpret_cast<const uint4*>(y + off);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float d[E], yy[E];
+      load_vec(reinterpret_cast<const T*>(&dv[u]), d);
+      if constexpr (HAS_OUT) {
+        float o[E];
+        load_vec(reinterpret_cast<const T*>(&ov[u]), o);
+#pragma unroll
+        for (int e = 0; e < E; ++e) d[e] = o[e] > 0.f ? d[e] : 0.f;
+      }
+      load_vec(reinterpret_cast<const T*>(&yv[u]), yy);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        s[e] += d[e];
+        q[e] = fmaf(d[e], (yy[e] - mu[e]) * iv[e], q[e]);
+      }
+    }
+  }
+  for (; r < r1; r += RL) {
     const int64_t off = r * C + c0;
     float d[E], yy[E];
     load_vec(dout + off, d);
-    if (out) {
+    if constexpr (HAS_OUT) {
       float o[E];
       load_vec(out + off, o);
 #pragma unroll
@@ -391,11 +422,11 @@ extern "C" int pose6d_bn_bwd(int32_t dtype, const void* dout, const void* out, c
   P6_CHECK_ARG(cpr % cl == 0 && kThreads % cl == 0, "pose6d_bn_bwd: C / vector width must be a power of two");
   dim3 grid(cpr / cl, nb);
   if (dtype == POSE6D_DT_BF16) {
-    bn_bwd_reduce2_kernel<bf16><<<grid, kThreads, 0, s>>>((const bf16*)dout, (const bf16*)out, (const bf16*)y, mean,
-                                                          invstd, part, M, C, rpb);
+    auto k = out ? bn_bwd_reduce2_kernel<bf16, true> : bn_bwd_reduce2_kernel<bf16, false>;
+    k<<<grid, kThreads, 0, s>>>((const bf16*)dout, (const bf16*)out, (const bf16*)y, mean, invstd, part, M, C, rpb);
   } else {
-    bn_bwd_reduce2_kernel<float><<<grid, kThreads, 0, s>>>((const float*)dout, (const float*)out, (const float*)y, mean,
-                                                           invstd, part, M, C, rpb);
+    auto k = out ? bn_bwd_reduce2_kernel<float, true> : bn_bwd_reduce2_kernel<float, false>;
+    k<<<grid, kThreads, 0, s>>>((const float*)dout, (const float*)out, (const float*)y, mean, invstd, part, M, C, rpb);
   }
   P6_LAUNCH_CHECK();
   bn_bwd_finalize_kernel<<<p6::ceil_div(C, 16), kThreads, 0, s>>>(part, nb, C, (double)M, gamma, invstd, dgamma, dbeta,

@@ -74,6 +74,6 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 
 inline hipStream_t stream_of(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
-inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+__host__ __device__ inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
 }  // namespace p6

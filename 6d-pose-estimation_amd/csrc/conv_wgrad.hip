@@ -421,41 +421,78 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_lds_kernel(const bf16* __
       }
 }
 
-// sum the split slabs (fixed order) into the OIHW fp32 gradient; k = (kh, kw, ci)
-// block = 32 consecutive (co, k) elements x 8 split-groups: each thread sums every
-// 8th slab (4 independent loads in flight), LDS combines the 8 groups in order.
+// sum the split slabs (fixed order) into the OIHW fp32 gradient; k = (kh, kw, ci).
+// Block = L float4 lanes (4 consecutive k each) x G split groups: group g sums
+// slabs g, g + G, ... with U loads in flight, then the G partials are combined in
+// LDS in group order (deterministic).  G is picked so that small gradients with
+// hundreds of splits still spread their reads over many lanes.
+template <int G>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw,
                                                            int Cout, int Kpad, int SC, int Cin, int KH, int KW,
                                                            int splits, int accumulate) {
-  __shared__ float red[8][33];
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  const int K = KH * KW * SC;
-  const int64_t idx = blockIdx.x * 32ll + tx;
-  const bool ok = idx < (int64_t)Cout * K;
-  const int co = ok ? (int)(idx / K) : 0, k = ok ? (int)(idx - (int64_t)co * K) : 0;
-  const int64_t slab = (int64_t)Cout * Kpad;
-  const float* p = ws + (int64_t)co * Kpad + k;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  int i = ty;
-  if (ok) {
-    for (; i + 24 < splits; i += 32) {
-      a0 += p[i * slab]; a1 += p[(i + 8) * slab]; a2 += p[(i + 16) * slab]; a3 += p[(i + 24) * slab];
-    }
-    for (; i < splits; i += 8) a0 += p[i * slab];
-  }
-  red[ty][tx] = (a0 + a1) + (a2 + a3);
-  __syncthreads();
-  if (ty == 0 && ok) {
-    float s = 0.f;
+  constexpr int L = 256 / G;
+  constexpr int U = 4;
+  __shared__ float4 red[G][L];
+  const int lane = threadIdx.x % L, grp = threadIdx.x / L;
+  const int64_t e0 = ((int64_t)blockIdx.x * L + lane) * 4;   // first of 4 consecutive (co, k) elements
+  const int64_t total = (int64_t)Cout * Kpad;
+  const bool ok = e0 < total;
+  const int64_t slab = total;
+  float4 acc[U];
 #pragma unroll
-    for (int g = 0; g < 8; ++g) s += red[g][tx];
-    const int tap = k / SC, ci = k - tap * SC;
-    if (ci < Cin) {
+  for (int u = 0; u < U; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ok) {
+    const float* p = ws + e0;
+    int i = grp;
+    for (; i + (U - 1) * G < splits; i += U * G) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const float4*>(p + (int64_t)(i + u * G) * slab);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        acc[u].x += v[u].x; acc[u].y += v[u].y; acc[u].z += v[u].z; acc[u].w += v[u].w;
+      }
+    }
+    for (; i < splits; i += G) {
+      const float4 v = *reinterpret_cast<const float4*>(p + (int64_t)i * slab);
+      acc[0].x += v.x; acc[0].y += v.y; acc[0].z += v.z; acc[0].w += v.w;
+    }
+  }
+  float4 t = acc[0];
+#pragma unroll
+  for (int u = 1; u < U; ++u) { t.x += acc[u].x; t.y += acc[u].y; t.z += acc[u].z; t.w += acc[u].w; }
+  red[grp][lane] = t;
+  __syncthreads();
+  if (grp == 0 && ok) {
+#pragma unroll
+    for (int g = 1; g < G; ++g) { const float4 v = red[g][lane]; t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w; }
+    const float tv[4] = {t.x, t.y, t.z, t.w};
+    const int co = (int)(e0 / Kpad), k0 = (int)(e0 - (int64_t)co * Kpad);
+    const int K = KH * KW * SC;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + j;
+      if (k >= K) continue;
+      const int tap = k / SC, ci = k - tap * SC;
+      if (ci >= Cin) continue;
       const int kh = tap / KW, kw = tap - kh * KW;
       float* d = dw + (((int64_t)co * Cin + ci) * KH + kh) * KW + kw;
-      *d = accumulate ? *d + s : s;
+      *d = accumulate ? *d + tv[j] : tv[j];
     }
   }
+}
+
+int launch_reduce(const float* ws, float* dw, int Cout, int Kpad, int SC, int Cin, int KH, int KW, int splits,
+                  int accumulate, hipStream_t s) {
+  const int64_t quads = (int64_t)Cout * Kpad / 4;
+  auto go = [&](auto kern, int L) {
+    kern<<<(unsigned)((quads + L - 1) / L), 256, 0, s>>>(ws, dw, Cout, Kpad, SC, Cin, KH, KW, splits, accumulate);
+  };
+  if (splits >= 64) go(wgrad_reduce_kernel<16>, 16);
+  else if (splits >= 16) go(wgrad_reduce_kernel<4>, 64);
+  else go(wgrad_reduce_kernel<1>, 256);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
 }
 
 struct Plan {
@@ -556,7 +593,7 @@ extern "C" int64_t pose6d_conv2d_wgrad_workspace(int32_t dtype, int32_t N, int32
 }
 
 extern "C" int pose6d_conv2d_wgrad(int32_t dtype, const void* x, const void* dy, float* dw, int32_t accumulate,
-                                   float* workspace, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cin_real,
+                                   float* workspace, int64_t ws_bytes, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cin_real,
                                    int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho,
                                    int32_t Wo, void* stream) {
   P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_wgrad: bad dtype %d", dtype);
@@ -571,6 +608,9 @@ extern "C" int pose6d_conv2d_wgrad(int32_t dtype, const void* x, const void* dy,
   const Plan p = plan(dtype, g.M, Cout, g.Kpad, Cin);
   g.gm = p6::ceil_div(Cout, p.bm); g.gn = p6::ceil_div(g.Kpad, p.bn);
   g.splits = p.splits; g.mps = p.mps;
+  P6_CHECK_ARG((int64_t)p.splits * Cout * g.Kpad * 4 <= ws_bytes,
+               "pose6d_conv2d_wgrad: workspace %lld bytes < %lld needed (query pose6d_conv2d_wgrad_workspace with the "
+               "same environment)", (long long)ws_bytes, (long long)p.splits * Cout * g.Kpad * 4);
   hipStream_t s = p6::stream_of(stream);
   int rc;
   if (p.fast) {
@@ -582,11 +622,7 @@ extern "C" int pose6d_conv2d_wgrad(int32_t dtype, const void* x, const void* dy,
                                  : launch_any<float>(g, p.bm, p.bn, x, dy, workspace, s);
   }
   if (rc) return rc;
-  const int64_t total = (int64_t)Cout * g.K;
-  wgrad_reduce_kernel<<<(unsigned)((total + 31) / 32), 256, 0, s>>>(workspace, dw, Cout, g.Kpad, Cin, Cin_real, KH,
-                                                                    KW, g.splits, accumulate);
-  P6_LAUNCH_CHECK();
-  return POSE6D_OK;
+  return launch_reduce(workspace, dw, Cout, g.Kpad, Cin, Cin_real, KH, KW, g.splits, accumulate, s);
 }
 
 // weight-gradient kernel variant: (stages << 12) | (fast << 8) | (BM == 128) << 1 | (BN == 128)

@@ -51,30 +51,56 @@ struct PackDesc {
   int64_t start, count;
 };
 
+// z = 0: wp[o][k], k = (kh, kw, ci): each OIHW row o is staged in LDS (coalesced
+//        row read), then written in (kh, kw, ci) order with channel / K padding.
+// z = 1: wt[(ci, kh, kw)][o] is the transpose of w viewed as [O][I*KH*KW]: 64 x 64
+//        tiles through LDS, coalesced on both sides.
+constexpr int kPackRow = 4608;   // largest staged row (512 x 3 x 3); longer rows gather directly
+
 template <typename T>
-__global__ void pack_kernel(const PackDesc* __restrict__ descs) {
+__global__ __launch_bounds__(kThreads) void pack_kernel(const PackDesc* __restrict__ descs) {
+  __shared__ float sm[kPackRow > 64 * 65 ? kPackRow : 64 * 65];
   const PackDesc d = descs[blockIdx.y];
-  const int64_t stride = (int64_t)gridDim.x * kThreads;
-  if (blockIdx.z == 0) {          // wp[o][k], k = (kh, kw, ci)
-    const int K = d.KH * d.KW * d.Ip;
-    for (int64_t j = blockIdx.x * (int64_t)kThreads + threadIdx.x; j < d.count; j += stride) {
-      const int o = (int)(j / d.Kpad), k = (int)(j - (int64_t)o * d.Kpad);
-      float v = 0.f;
-      if (k < K) {
-        const int tap = k / d.Ip, c = k - tap * d.Ip, kh = tap / d.KW, kw = tap - kh * d.KW;
-        if (c < d.I) v = d.w[(((int64_t)o * d.I + c) * d.KH + kh) * d.KW + kw];
+  const int taps = d.KH * d.KW;
+  const int R = d.I * taps;
+  if (blockIdx.z == 0) {
+    const int K = taps * d.Ip;
+    for (int o = blockIdx.x; o < d.O; o += gridDim.x) {
+      const float* row = d.w + (int64_t)o * R;
+      const bool staged = R <= kPackRow;
+      if (staged) {
+        for (int r = threadIdx.x; r < R; r += kThreads) sm[r] = row[r];
+        __syncthreads();
       }
-      reinterpret_cast<T*>(d.wp)[j] = p6::from_f<T>(v);
+      T* dst = reinterpret_cast<T*>(d.wp) + (int64_t)o * d.Kpad;
+      for (int k = threadIdx.x; k < d.Kpad; k += kThreads) {
+        float v = 0.f;
+        if (k < K) {
+          const int tap = k / d.Ip, c = k - tap * d.Ip;
+          if (c < d.I) v = staged ? sm[c * taps + tap] : row[c * taps + tap];
+        }
+        dst[k] = p6::from_f<T>(v);
+      }
+      __syncthreads();
     }
-  } else if (d.wt) {              // wt[c][kh][kw][o]
-    const int64_t n = (int64_t)d.I * d.KH * d.KW * d.O;
-    for (int64_t j = blockIdx.x * (int64_t)kThreads + threadIdx.x; j < n; j += stride) {
-      const int o = (int)(j % d.O);
-      int64_t r = j / d.O;
-      const int kw = (int)(r % d.KW); r /= d.KW;
-      const int kh = (int)(r % d.KH);
-      const int c = (int)(r / d.KH);
-      reinterpret_cast<T*>(d.wt)[j] = p6::from_f<T>(d.w[(((int64_t)o * d.I + c) * d.KH + kh) * d.KW + kw]);
+  } else if (d.wt) {
+    const int tr = p6::ceil_div(R, 64), to = p6::ceil_div(d.O, 64);
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int t = blockIdx.x; t < tr * to; t += gridDim.x) {
+      const int o0 = (t / tr) * 64, r0 = (t - (t / tr) * tr) * 64;
+#pragma unroll 4
+      for (int i = ty; i < 64; i += 4) {   // rows o0 + i of w, columns r0 + tx
+        const int o = o0 + i, r = r0 + tx;
+        sm[i * 65 + tx] = (o < d.O && r < R) ? d.w[(int64_t)o * R + r] : 0.f;
+      }
+      __syncthreads();
+      T* wt = reinterpret_cast<T*>(d.wt);
+#pragma unroll 4
+      for (int i = ty; i < 64; i += 4) {   // rows r0 + i of wt, columns o0 + tx
+        const int r = r0 + i, o = o0 + tx;
+        if (r < R && o < d.O) wt[(int64_t)r * d.O + o] = p6::from_f<T>(sm[tx * 65 + i]);
+      }
+      __syncthreads();
     }
   }
 }

@@ -54,8 +54,8 @@ def conv_launches(eng):
         dw = torch.empty_like(op.conv.weight)
 
         def wgrad(op=op, dw=dw):
-            call("conv2d_wgrad", dt, op.src.t, op.out.g, dw, 0, eng.ws_wgrad, B, op.H, op.W, op.cin_pad, op.cin,
-                 op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, st)
+            call("conv2d_wgrad", dt, op.src.t, op.out.g, dw, 0, eng.ws_wgrad, eng.ws_wgrad.numel() * 4, B, op.H,
+                 op.W, op.cin_pad, op.cin, op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, st)
         out.append((sym + "+reduce", flops, wgrad, op.name + ".wgrad"))
     return out
 

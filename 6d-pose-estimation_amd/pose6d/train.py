@@ -169,7 +169,7 @@ class RGBDGeometricTrainer:
                 end = self.bucket_ends[state["next"]][1]
                 s = state["start"]
                 ev = torch.cuda.Event()
-                ev.record(cur)
+                ev.record(torch.cuda.current_stream())   # the stream that finished the gradients
                 with torch.cuda.stream(comm):
                     comm.wait_event(ev)
                     handles.append(dist.all_reduce(self.arena.grad[s:end], group=self.pg, async_op=True))

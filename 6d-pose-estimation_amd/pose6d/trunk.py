@@ -17,6 +17,8 @@ differentiates (checked with a generation counter).
 """
 import ctypes
 
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -284,6 +286,8 @@ class TrunkEngine:
         if self._saved_gen != self.generation:
             raise Pose6dError("TrunkEngine.backward: activations of the matching training forward were overwritten")
         st = stream()
+        main = torch.cuda.current_stream()
+        side = self._side_stream() if os.environ.get("POSE6D_WGRAD_SIDE", "0") == "1" else main
         dt = self.dt
         B = self.B
         acc = int(accumulate)
@@ -311,10 +315,21 @@ class TrunkEngine:
             elif isinstance(op, _ConvOp):
                 dy = op.out.g
                 M = B * op.Ho * op.Wo
-                call("conv2d_wgrad", dt, op.src.t, dy, grad_of(op.conv.weight), acc, self.ws_wgrad, B, op.H, op.W,
-                     op.cin_pad, op.cin, op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, st)
-                if op.conv.bias is not None:
-                    call("channel_sum", dt, dy, M, op.cout, grad_of(op.conv.bias), acc, st)
+                # the weight gradient is off the critical path: it runs on the side
+                # stream (its own workspace, in order there) beside the data gradient
+                if side is not main:
+                    ev = torch.cuda.Event()
+                    ev.record(main)
+                    side.wait_event(ev)
+                with torch.cuda.stream(side):
+                    sst = stream()
+                    call("conv2d_wgrad", dt, op.src.t, dy, grad_of(op.conv.weight), acc, self.ws_wgrad,
+                         self.ws_wgrad.numel() * 4, B, op.H, op.W, op.cin_pad, op.cin, op.cout, op.k, op.k,
+                         op.stride, op.pad, op.Ho, op.Wo, sst)
+                    if op.conv.bias is not None:
+                        call("channel_sum", dt, dy, M, op.cout, grad_of(op.conv.bias), acc, sst)
+                    if on_conv_done is not None:
+                        on_conv_done(op)   # records its event on the side stream
                 if op.needs_dgrad:
                     src = op.src
                     if src.pending is not None and src.g is not None and src.pending is not src.g:
@@ -330,12 +345,17 @@ class TrunkEngine:
                     else:
                         call("conv2d_dgrad", dt, dy, op.wt, None, src.g, B, op.H, op.W, op.cin_pad, op.cout, op.k,
                              op.k, op.stride, op.pad, op.Ho, op.Wo, st)
-                if on_conv_done is not None:
-                    on_conv_done(op)
             else:
                 s = op.src
                 call("maxpool_bwd", dt, op.out.g, op.argmax, s.g, B, s.H, s.W, s.C, op.k, op.s, op.p, op.out.H,
                      op.out.W, st)
+        if side is not main:
+            main.wait_stream(side)   # every weight gradient is final when backward returns
+
+    def _side_stream(self):
+        if getattr(self, "_side", None) is None or self._side.device != torch.cuda.current_stream().device:
+            self._side = torch.cuda.Stream(device=torch.cuda.current_stream().device)
+        return self._side
 
     def _has_later_consumer(self, op):
         """True if op.src is also consumed by a conv processed later in backward

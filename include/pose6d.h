@@ -138,11 +138,12 @@ int pose6d_conv2d_dgrad(int32_t dtype, const void *dy, const void *wt, const voi
                         int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
                         int32_t pad, int32_t Ho, int32_t Wo, void *stream);
 /* weight gradient into OIHW fp32 dw (Cin_real channels of the Cin-padded input);
- * workspace: pose6d_conv2d_wgrad_workspace(...) bytes of fp32 split slabs. */
+ * workspace: pose6d_conv2d_wgrad_workspace(...) bytes of fp32 split slabs, its
+ * size passed as ws_bytes (a plan needing more fails with POSE6D_EINVAL). */
 int64_t pose6d_conv2d_wgrad_workspace(int32_t dtype, int32_t N, int32_t Ho, int32_t Wo, int32_t Cin, int32_t Cout,
                                       int32_t KH, int32_t KW);
 int pose6d_conv2d_wgrad(int32_t dtype, const void *x, const void *dy, float *dw, int32_t accumulate,
-                        float *workspace, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cin_real,
+                        float *workspace, int64_t ws_bytes, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cin_real,
                         int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
                         void *stream);
 

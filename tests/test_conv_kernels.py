@@ -92,10 +92,12 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
         _close(dx.permute(0, 3, 1, 2), xr.grad + dres.float().cpu().permute(0, 3, 1, 2), tol, "dgrad(+res)")
     ws = torch.empty(query("conv2d_wgrad_workspace", dt, N, Ho, Wo, cpad, Cout, k, k) // 4 + 1, device=dev)
     dw = torch.full((Cout, Cin, k, k), 7.0, device=dev)
-    call("conv2d_wgrad", dt, xd, dyd, dw, 0, ws, N, H, W, cpad, Cin, Cout, k, k, s, p, Ho, Wo, stream())
+    call("conv2d_wgrad", dt, xd, dyd, dw, 0, ws, ws.numel() * 4, N, H, W, cpad, Cin, Cout, k, k, s, p, Ho, Wo,
+         stream())
     _close(dw, wr.grad, tol, "wgrad")
     dw2 = dw.clone()
-    call("conv2d_wgrad", dt, xd, dyd, dw2, 1, ws, N, H, W, cpad, Cin, Cout, k, k, s, p, Ho, Wo, stream())
+    call("conv2d_wgrad", dt, xd, dyd, dw2, 1, ws, ws.numel() * 4, N, H, W, cpad, Cin, Cout, k, k, s, p, Ho, Wo,
+         stream())
     _close(dw2, 2 * wr.grad, tol, "wgrad accumulate")
     if has_bias:
         db = torch.empty(Cout, device=dev)
@@ -139,7 +141,8 @@ def test_conv_fast_variants_bit_identical(cfg, monkeypatch):
         dw = torch.empty(Cout, Cin, k, k, device=dev)
         call("conv2d_fwd", dt, x, wp, None, y, None, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream())
         call("conv2d_dgrad", dt, dy, wt, dres, dx, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream())
-        call("conv2d_wgrad", dt, x, dy, dw, 0, ws, N, H, W, Cin, Cin, Cout, k, k, s, p, Ho, Wo, stream())
+        call("conv2d_wgrad", dt, x, dy, dw, 0, ws, ws.numel() * 4, N, H, W, Cin, Cin, Cout, k, k, s, p, Ho, Wo,
+             stream())
         torch.cuda.synchronize()
         return y.cpu(), dx.cpu(), dw.cpu()
 

@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--impls", default="base,fast")
     ap.add_argument("--tiles", default="auto,0,1,3")
     ap.add_argument("--stages", default="auto", help="fast-path LDS ring depths to sweep, e.g. auto,2,3,4,6")
+    ap.add_argument("--wgrad-env", default="", help="';'-separated K=V[,K=V] settings to sweep for wgrad")
     ap.add_argument("--B", type=int, default=32)
     a = ap.parse_args()
     B, dt, dtype, dev = a.B, DTYPES[torch.bfloat16], torch.bfloat16, "cuda"
@@ -57,17 +58,29 @@ def main():
         dy = torch.randn(B, Ho, Wo, Cout, device=dev).to(dtype)
         dx = torch.empty(B, H, W, Cin, device=dev, dtype=dtype)
         stats = torch.empty(query("conv_stats_rows", B, Ho, Wo, Cout), 2, Cout, device=dev)
-        ws = torch.empty(query("conv2d_wgrad_workspace", dt, B, Ho, Wo, Cin, Cout, k, k) // 4 + 1, device=dev)
+        # room for any split plan the --wgrad-env sweep selects (the call checks the size)
+        ws = torch.empty(max(query("conv2d_wgrad_workspace", dt, B, Ho, Wo, Cin, Cout, k, k), 256 << 20) // 4,
+                         device=dev)
         dw = torch.empty(Cout, Cin, k, k, device=dev)
         flops = 2.0 * B * Ho * Wo * Cout * Cin * k * k
         fns = {
             "fwd": lambda: call("conv2d_fwd", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, st),
             "dgrad": lambda: call("conv2d_dgrad", dt, dy, wt, None, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, st),
-            "wgrad": lambda: call("conv2d_wgrad", dt, x, dy, dw, 0, ws, B, H, W, Cin, Cin, Cout, k, k, s, p, Ho, Wo,
-                                  st),
+            "wgrad": lambda: call("conv2d_wgrad", dt, x, dy, dw, 0, ws, ws.numel() * 4, B, H, W, Cin, Cin, Cout, k, k,
+                                  s, p, Ho, Wo, st),
         }
         line = f"{H:3d}x{W:<3d} {Cin:4d}->{Cout:<4d} k{k}s{s} |"
         for ps in a.passes.split(","):
+            if ps == "wgrad" and a.wgrad_env:
+                for spec in ["auto"] + a.wgrad_env.split(";"):
+                    kv = [] if spec == "auto" else [e.split("=") for e in spec.split(",")]
+                    for k_, v_ in kv:
+                        os.environ[k_] = v_
+                    sec = timeit(fns[ps])
+                    for k_, _ in kv:
+                        os.environ.pop(k_, None)
+                    line += f" w[{spec}]:{sec * 1e6:6.1f}us/{flops / sec / 1e12:5.0f}T"
+                continue
             impls = a.impls.split(",") if ps != "wgrad" else ["base"]
             tiles = a.tiles.split(",") if ps != "wgrad" else ["auto"]
             for impl in impls:
