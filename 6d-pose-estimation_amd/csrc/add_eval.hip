@@ -169,6 +169,99 @@ __global__ __launch_bounds__(kThreads) void add_reduce_kernel(
   }
 }
 
+// ---------------------------------------------------------------- ADD loss backward
+// d loss / d (pred_rot, pred_trans) of ADDLoss.forward (add_loss.py:101-150):
+//   loss = (1 / count) sum_i mean_k ||Q_ik - G*_ik||,  Q = P R(q)^T + t,
+//   G* = G_k (ADD) or G_argmin(k) (ADD-S: torch.min routes the gradient to the
+//   first-index minimum the forward found).  ||.|| backward is 0 at distance 0
+//   (torch's norm backward).  One block per sample: fp64 block sums of
+//   g = (Q - G*) / d and g P^T, then the chain rule through _quat_to_mat.
+__global__ __launch_bounds__(kThreads) void add_loss_bwd_kernel(
+    const float* __restrict__ pred_rot, const float* __restrict__ pred_trans, const float* __restrict__ gt_rot,
+    const float* __restrict__ gt_trans, const int64_t* __restrict__ obj_ids, int B, const float* __restrict__ points,
+    const int32_t* __restrict__ off, const int32_t* __restrict__ npts, const uint8_t* __restrict__ sym, int n_slots,
+    int max_npts, const int32_t* __restrict__ argmin, const float* __restrict__ dloss, float* __restrict__ grad_rot,
+    float* __restrict__ grad_trans) {
+  __shared__ double red[12][kThreads / 64];
+  __shared__ int cnt_s;
+  const int b = blockIdx.x;
+  const int64_t oid = obj_ids[b];
+  const int n = (oid >= 0 && oid < n_slots) ? npts[oid] : 0;
+  // count of samples that enter the loss (known objects with points)
+  int c = 0;
+  for (int i = threadIdx.x; i < B; i += kThreads) {
+    const int64_t o = obj_ids[i];
+    c += (o >= 0 && o < n_slots && npts[o] > 0) ? 1 : 0;
+  }
+  c = (int)p6::wave_sum((float)c);
+  if (threadIdx.x == 0) cnt_s = 0;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) atomicAdd(&cnt_s, c);
+  __syncthreads();
+  if (n <= 0) {
+    if (threadIdx.x < 4) grad_rot[4 * b + threadIdx.x] = 0.f;
+    if (threadIdx.x < 3) grad_trans[3 * b + threadIdx.x] = 0.f;
+    return;
+  }
+  const Mat3 Rp = quat_to_mat(pred_rot + 4 * b);
+  const Mat3 Rg = quat_to_mat(gt_rot + 4 * b);
+  const float* tp = pred_trans + 3 * b;
+  const float* tg = gt_trans + 3 * b;
+  const float* P = points + 3 * (int64_t)off[oid];
+  const bool is_sym = sym[oid] != 0;
+  double acc[12];   // gt[3], gR[3][3] (row a = output coordinate, col = point coordinate)
+#pragma unroll
+  for (int i = 0; i < 12; ++i) acc[i] = 0.0;
+  for (int k = threadIdx.x; k < n; k += kThreads) {
+    const float4 q = xform(P + 3 * k, Rp, tp, n);
+    const int j = is_sym ? argmin[(int64_t)b * max_npts + k] : k;
+    const float4 g = xform(P + 3 * j, Rg, tg, n);
+    const float dx = q.x - g.x, dy = q.y - g.y, dz = q.z - g.z;
+    const float d = sqrtf(fmaf(dz, dz, fmaf(dy, dy, dx * dx)));
+    if (!(d > 0.f)) continue;
+    const double gx = dx / d, gy = dy / d, gz = dz / d;
+    const double p0 = P[3 * k], p1 = P[3 * k + 1], p2 = P[3 * k + 2];
+    acc[0] += gx; acc[1] += gy; acc[2] += gz;
+    acc[3] += gx * p0; acc[4] += gx * p1; acc[5] += gx * p2;
+    acc[6] += gy * p0; acc[7] += gy * p1; acc[8] += gy * p2;
+    acc[9] += gz * p0; acc[10] += gz * p1; acc[11] += gz * p2;
+  }
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const double v = p6::wave_sum(acc[i]);
+    if ((threadIdx.x & 63) == 0) red[i][w] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  double t[12];
+  const double scale = (double)dloss[0] / ((double)cnt_s * (double)n);
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    double v = 0.0;
+    for (int k = 0; k < kThreads / 64; ++k) v += red[i][k];
+    t[i] = v * scale;
+  }
+  grad_trans[3 * b + 0] = (float)t[0];
+  grad_trans[3 * b + 1] = (float)t[1];
+  grad_trans[3 * b + 2] = (float)t[2];
+  const double* G = t + 3;   // dL/dR[a][c], row-major r0..r8
+  const double x = pred_rot[4 * b], y = pred_rot[4 * b + 1], z = pred_rot[4 * b + 2], ww = pred_rot[4 * b + 3];
+  // d r / d(x, y, z, w) of add_loss.py:203-215
+  const double drx[9] = {0, 2 * y, 2 * z, 2 * y, -4 * x, -2 * ww, 2 * z, 2 * ww, -4 * x};
+  const double dry[9] = {-4 * y, 2 * x, 2 * ww, 2 * x, 0, 2 * z, -2 * ww, 2 * z, -4 * y};
+  const double drz[9] = {-4 * z, -2 * ww, 2 * x, 2 * ww, -4 * z, 2 * y, 2 * x, 2 * y, 0};
+  const double drw[9] = {0, -2 * z, 2 * y, 2 * z, 0, -2 * x, -2 * y, 2 * x, 0};
+  double gq[4] = {0, 0, 0, 0};
+  for (int i = 0; i < 9; ++i) {
+    gq[0] += G[i] * drx[i];
+    gq[1] += G[i] * dry[i];
+    gq[2] += G[i] * drz[i];
+    gq[3] += G[i] * drw[i];
+  }
+  for (int i = 0; i < 4; ++i) grad_rot[4 * b + i] = (float)gq[i];
+}
+
 }  // namespace
 
 extern "C" int pose6d_add_eval(const float* pred_rot, const float* pred_trans, const float* gt_rot,
@@ -190,6 +283,21 @@ extern "C" int pose6d_add_eval(const float* pred_rot, const float* pred_trans, c
   }
   add_reduce_kernel<<<(unsigned)B, kThreads, 0, s>>>(obj_ids, npts, sym, diam, n_slots, max_npts, min_dist, pt_add,
                                                       add, adds, valid, correct);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+extern "C" int pose6d_add_loss_bwd(const float* pred_rot, const float* pred_trans, const float* gt_rot,
+                                   const float* gt_trans, const int64_t* obj_ids, int64_t B, const float* points,
+                                   const int32_t* off, const int32_t* npts, const uint8_t* sym, int32_t n_slots,
+                                   int32_t max_npts, const int32_t* argmin, const float* dloss, float* grad_rot,
+                                   float* grad_trans, void* stream) {
+  P6_CHECK_ARG(B >= 0 && B <= 65535, "pose6d_add_loss_bwd: batch %lld out of range", (long long)B);
+  P6_CHECK_ARG(argmin && dloss && grad_rot && grad_trans, "pose6d_add_loss_bwd: null argument");
+  if (B == 0) return POSE6D_OK;
+  add_loss_bwd_kernel<<<(unsigned)B, kThreads, 0, p6::stream_of(stream)>>>(
+      pred_rot, pred_trans, gt_rot, gt_trans, obj_ids, (int)B, points, off, npts, sym, n_slots, max_npts, argmin,
+      dloss, grad_rot, grad_trans);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }

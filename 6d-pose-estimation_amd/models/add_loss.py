@@ -151,21 +151,50 @@ class ADDLoss(nn.Module):
         if pred_r.shape[0] == 0:
             return {"add_mean": 0, "add_s_mean": 0, "add_01d_acc": 0}
         s = self.per_sample(pred_r, pred_t, gt_r, gt_t, obj_ids)
-        host = torch.stack([s["add"], s["adds"], s["valid"].double(), s["correct"].double()]).cpu().numpy()
+        return self.aggregate(s["add"], s["adds"], s["valid"], s["correct"])
+
+    @staticmethod
+    def aggregate(add, adds, valid, correct):
+        """The eval_metrics dict from per-sample results (add_loss.py:197-201)."""
+        host = torch.stack([add.double(), adds.double(), valid.double(), correct.double()]).cpu().numpy()
         v = host[2] > 0
-        add, adds, corr = host[0][v].tolist(), host[1][v].tolist(), host[3][v].tolist()
+        a, s_, c = host[0][v].tolist(), host[1][v].tolist(), host[3][v].tolist()
         return {
-            "add_mean": np.mean(add) * 1000 if add else 0,
-            "add_s_mean": np.mean(adds) * 1000 if adds else 0,
-            "add_01d_acc": np.mean(corr) * 100 if corr else 0,
+            "add_mean": np.mean(a) * 1000 if a else 0,
+            "add_s_mean": np.mean(s_) * 1000 if s_ else 0,
+            "add_01d_acc": np.mean(c) * 100 if c else 0,
         }
+
+    @torch.no_grad()
+    def eval_metrics_sharded(self, pred_r, pred_t, gt_r, gt_t, obj_ids, group=None):
+        """eval_metrics over a batch split across the ranks of `group` (SURVEY.md
+        §8e): every rank evaluates its own samples on its GPU, the per-sample
+        (ADD, ADD-S, valid, correct) are all-gathered in rank order and every
+        rank returns the dict eval_metrics would give for the concatenated batch."""
+        from pose6d.dist import gather_samples
+        if pred_r.shape[0] > 0:
+            s = self.per_sample(pred_r, pred_t, gt_r, gt_t, obj_ids)
+            parts = [s["add"], s["adds"], s["valid"], s["correct"]]
+        else:
+            dev = pred_r.device
+            parts = [torch.zeros(0, dtype=torch.float64, device=dev), torch.zeros(0, dtype=torch.float64, device=dev),
+                     torch.zeros(0, dtype=torch.int32, device=dev), torch.zeros(0, dtype=torch.int32, device=dev)]
+        add, adds, valid, correct = gather_samples(parts, group)
+        if add.shape[0] == 0:
+            return {"add_mean": 0, "add_s_mean": 0, "add_01d_acc": 0}
+        return self.aggregate(add, adds, valid, correct)
 
     def forward(self, pred_r, pred_t, gt_r, gt_t, obj_ids):
         """add_loss.py:101-150: mean over known samples of ADD (ADD-S for symmetric
-        objects).  Returned as a device scalar; no gradient."""
+        objects), a device scalar differentiable w.r.t. pred_r / pred_t
+        (pose6d_add_loss_bwd; ADD-S routes the gradient through the first-index
+        nearest point, as torch.min does)."""
         if pred_r.shape[0] == 0:
             return torch.tensor(0.0, device=pred_r.device, requires_grad=True)
-        s = self.per_sample(pred_r, pred_t, gt_r, gt_t, obj_ids)
+        return _ADDLossFn.apply(pred_r, pred_t, gt_r, gt_t, obj_ids, self)
+
+    def _loss_forward(self, pred_r, pred_t, gt_r, gt_t, obj_ids):
+        s = self.per_sample(pred_r, pred_t, gt_r, gt_t, obj_ids, want_points=True)
         T = self._table
         ids = obj_ids.detach().to(torch.int64)
         known = (ids >= 0) & (ids < max(T.n_slots, 1))
@@ -175,8 +204,31 @@ class ADDLoss(nn.Module):
         v = s["valid"] > 0
         cnt = v.sum()
         tot = torch.where(v, per, torch.zeros_like(per)).sum()
-        return torch.where(cnt > 0, tot / cnt.clamp_min(1), torch.zeros_like(tot)).to(torch.float32)
+        loss = torch.where(cnt > 0, tot / cnt.clamp_min(1), torch.zeros_like(tot)).to(torch.float32)
+        return loss, s["argmin"]
 
     def train_loss(self, pred_r, pred_t, gt_r, gt_t, obj_ids):
         """Alias for forward() (add_loss.py:152-154)."""
         return self.forward(pred_r, pred_t, gt_r, gt_t, obj_ids)
+
+
+class _ADDLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred_r, pred_t, gt_r, gt_t, obj_ids, mod):
+        loss, argmin = mod._loss_forward(pred_r, pred_t, gt_r, gt_t, obj_ids)
+        f = lambda t: t.detach().to(torch.float32).contiguous()
+        ctx.save_for_backward(f(pred_r), f(pred_t), f(gt_r), f(gt_t), obj_ids.detach().to(torch.int64).contiguous(),
+                              argmin)
+        ctx.mod = mod
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        pr, pt, gr, gt, ids, argmin = ctx.saved_tensors
+        T = ctx.mod._table
+        B = pr.shape[0]
+        grad_r = torch.empty(B, 4, device=pr.device, dtype=torch.float32)
+        grad_t = torch.empty(B, 3, device=pr.device, dtype=torch.float32)
+        call("add_loss_bwd", pr, pt, gr, gt, ids, B, T.points, T.off, T.npts, T.sym, T.n_slots, T.max_npts, argmin,
+             dloss.detach().to(torch.float32).reshape(1).contiguous(), grad_r, grad_t, stream())
+        return grad_r, grad_t, None, None, None, None

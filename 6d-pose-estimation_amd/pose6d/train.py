@@ -21,6 +21,7 @@ import math
 import torch
 
 from ._lib import call, stream
+from .dist import BucketReducer, plan_buckets
 from .head import HeadEngine
 from .trunk import TrunkEngine
 
@@ -104,15 +105,10 @@ class RGBDGeometricTrainer:
         self.bucket_ends = []
         if self.world == 1:
             return
-        limit = int(bucket_mb * 1e6 / 4)
-        start = 0
-        for p, off in zip(self.arena.params, self.arena.offsets):
-            end = off + p.numel()
-            if end - start >= limit:
-                self.bucket_ends.append((p, end))
-                start = end
-        if not self.bucket_ends or self.bucket_ends[-1][1] != self.arena.numel:
-            self.bucket_ends.append((self.arena.params[-1], self.arena.numel))
+        sizes = [(off, p.numel()) for p, off in zip(self.arena.params, self.arena.offsets)]
+        ends = plan_buckets(sizes, int(bucket_mb * 1e6 / 4))
+        ends[-1] = (ends[-1][0], self.arena.numel)   # the last bucket covers the alignment tail
+        self.bucket_ends = [(self.arena.params[i], e) for i, e in ends]
 
     # ------------------------------------------------------------- the step
     def _forward_loss(self, rgb, depth_raw, bbox, K, gt_rot, gt_trans):
@@ -157,36 +153,16 @@ class RGBDGeometricTrainer:
         """Trunk backward with bucketed all-reduce: when the conv that completes a
         bucket is done, the bucket's all-reduce is enqueued on the comm stream
         (ordered after that point by an event) and overlaps the rest of backward."""
-        import torch.distributed as dist
-        comm = self._comm_stream()
-        handles = []
-        state = {"start": 0, "next": 0}
-        cur = torch.cuda.current_stream()
-
-        def issue_upto(done):
-            # every bucket whose end lies within the completed prefix [0, done)
-            while state["next"] < len(self.bucket_ends) and self.bucket_ends[state["next"]][1] <= done:
-                end = self.bucket_ends[state["next"]][1]
-                s = state["start"]
-                ev = torch.cuda.Event()
-                ev.record(torch.cuda.current_stream())   # the stream that finished the gradients
-                with torch.cuda.stream(comm):
-                    comm.wait_event(ev)
-                    handles.append(dist.all_reduce(self.arena.grad[s:end], group=self.pg, async_op=True))
-                state["start"] = end
-                state["next"] += 1
+        red = BucketReducer(self.arena.grad, self.bucket_ends, self.pg, self._comm_stream())
 
         def on_conv(op):
             # gradients complete in arena order: after this conv, everything up to its
             # last parameter (weight, or bias if it has one) is final
             last = op.conv.bias if op.conv.bias is not None else op.conv.weight
-            issue_upto(self.arena.end_offset(last))
+            red.ready(self.arena.end_offset(last))
 
         self.trunk.backward(dfeat, self.arena.grad_of, on_conv_done=on_conv)
-        issue_upto(self.arena.numel)
-        for h in handles:
-            h.wait()
-        cur.wait_stream(comm)
+        red.finish()
 
     def _comm_stream(self):
         if not hasattr(self, "_comm"):

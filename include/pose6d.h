@@ -62,6 +62,18 @@ int pose6d_add_eval(const float *pred_rot, const float *pred_trans, const float 
                     float *min_dist, int32_t *argmin, float *pt_add,
                     double *add, double *adds, int32_t *valid, int32_t *correct, void *stream);
 
+/* Backward of ADDLoss.forward (add_loss.py:101-150) w.r.t. the predicted pose:
+ * loss = mean over known samples of mean_k ||Q_k - G*_k|| (G* = G_k, or the
+ * nearest ground-truth point for SYMMETRIC_OBJECT_IDS, taken from the `argmin`
+ * [B][max_npts] a pose6d_add_eval call on the same inputs produced); dloss is a
+ * device scalar.  grad_rot [B][4] (through _quat_to_mat, add_loss.py:203-215),
+ * grad_trans [B][3]; unknown objects get zero gradient. */
+int pose6d_add_loss_bwd(const float *pred_rot, const float *pred_trans, const float *gt_rot,
+                        const float *gt_trans, const int64_t *obj_ids, int64_t B, const float *points,
+                        const int32_t *off, const int32_t *npts, const uint8_t *sym, int32_t n_slots,
+                        int32_t max_npts, const int32_t *argmin, const float *dloss, float *grad_rot,
+                        float *grad_trans, void *stream);
+
 /* ------------------------------------------------------------------------
  * Pose heads and loss
  * ---------------------------------------------------------------------- */

@@ -131,6 +131,44 @@ def forward(points, pred_r, pred_t, gt_r, gt_t, obj_ids):
     return 0.0 if count == 0 else total / count
 
 
+def forward_torch(points, pred_r, pred_t, gt_r, gt_t, obj_ids):
+    """add_loss.py:101-150 restated with torch ops (differentiable: the gradient
+    reference for pose6d_add_loss_bwd).  points: dict oid -> (N, 3) fp32 tensor;
+    groups by object in first-appearance order as the reference does."""
+    import torch
+
+    def q2m(q):   # add_loss.py:203-215
+        x, y, z, w = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+        x2, y2, z2 = x * x, y * y, z * z
+        xy, xz, yz = x * y, x * z, y * z
+        wx, wy, wz = w * x, w * y, w * z
+        r0 = torch.stack([1 - 2 * y2 - 2 * z2, 2 * xy - 2 * wz, 2 * xz + 2 * wy], dim=1)
+        r1 = torch.stack([2 * xy + 2 * wz, 1 - 2 * x2 - 2 * z2, 2 * yz - 2 * wx], dim=1)
+        r2 = torch.stack([2 * xz - 2 * wy, 2 * yz + 2 * wx, 1 - 2 * x2 - 2 * y2], dim=1)
+        return torch.stack([r0, r1, r2], dim=1)
+
+    pR, gR = q2m(pred_r), q2m(gt_r)
+    groups = {}
+    for i in range(pred_r.shape[0]):
+        oid = int(obj_ids[i])
+        if oid in points:
+            groups.setdefault(oid, []).append(i)
+    total = torch.zeros((), dtype=pred_r.dtype)
+    count = 0
+    for oid, idx in groups.items():
+        idx = torch.tensor(idx, dtype=torch.long)
+        P = points[oid].to(pred_r.dtype)
+        G = torch.matmul(P.unsqueeze(0), gR[idx].transpose(-1, -2)) + gt_t[idx].unsqueeze(1)
+        Q = torch.matmul(P.unsqueeze(0), pR[idx].transpose(-1, -2)) + pred_t[idx].unsqueeze(1)
+        if oid in SYMMETRIC_OBJECT_IDS:
+            per = torch.norm(Q.unsqueeze(2) - G.unsqueeze(1), dim=3).min(dim=2)[0].mean(dim=1)
+        else:
+            per = torch.norm(Q - G, dim=2).mean(dim=1)
+        total = total + per.sum()
+        count += len(idx)
+    return total / count if count else total
+
+
 def load_models(model_dir, num_points=500):
     """add_loss.py:29-99 (loader), including its quirks: every post-header line
     with >= 3 tokens is a vertex, diameters from models_info.yml (mm -> m),

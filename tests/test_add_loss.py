@@ -103,3 +103,49 @@ def test_add_eval_c4_full_size_vs_oracle():
     s2 = crit.per_sample(*args2, want_points=True)
     assert float(s2["min"].abs().max()) == 0.0
     assert float(s2["adds"].abs().max()) == 0.0
+
+
+def test_oracle_torch_forward_matches_reference_goldens(golden):
+    """The differentiable torch restatement of ADDLoss.forward (the gradient
+    reference) reproduces the reference's own forward values (golden vectors)."""
+    from oracle import add_loss as OA
+    g = golden["add_loss"]
+    crit = _make("cpu")
+    for tag in ("n500", "n2000", "ties"):
+        if f"{tag}/forward" not in g:
+            continue
+        pts = dict(crit.points)
+        if tag != "n500":
+            for o in LINEMOD_OBJ_IDS:
+                pts[o] = torch.from_numpy(g[f"{tag}/points/{o}"])
+        args = _args(g, tag, "cpu")
+        v = OA.forward_torch(pts, *args).item()
+        np.testing.assert_allclose(v, g[f"{tag}/forward"], rtol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", ["n500", "n2000"])
+def test_add_loss_backward_vs_torch_autograd(golden, tag):
+    """ADDLoss.forward(...).backward(): gradients w.r.t. the predicted pose vs torch
+    autograd through the torch restatement of add_loss.py:101-150 (fp32, 1e-4)."""
+    from oracle import add_loss as OA
+    g = golden["add_loss"]
+    crit = _make("cuda")
+    pts = {o: v.cpu() for o, v in crit.points.items()}
+    if tag != "n500":
+        for o in LINEMOD_OBJ_IDS:
+            crit.points[o] = torch.from_numpy(g[f"{tag}/points/{o}"]).cuda()
+            pts[o] = torch.from_numpy(g[f"{tag}/points/{o}"])
+    pr, pt, gr, gt, ids = _args(g, tag, "cpu")
+    pr_d, pt_d = pr.cuda().requires_grad_(True), pt.cuda().requires_grad_(True)
+    loss = crit(pr_d, pt_d, gr.cuda(), gt.cuda(), ids.cuda())
+    loss.backward()
+    pr_r, pt_r = pr.clone().requires_grad_(True), pt.clone().requires_grad_(True)
+    ref = OA.forward_torch(pts, pr_r, pt_r, gr, gt, ids)
+    ref.backward()
+    np.testing.assert_allclose(loss.item(), ref.item(), rtol=1e-5)
+    for got, exp, what in ((pr_d.grad, pr_r.grad, "d pred_rot"), (pt_d.grad, pt_r.grad, "d pred_trans")):
+        got, exp = got.cpu(), exp
+        scale = exp.abs().max().item() + 1e-30
+        err = (got - exp).abs().max().item()
+        assert err <= 1e-4 * scale, f"{what}: max err {err:.3e} vs scale {scale:.3e}"

@@ -170,11 +170,14 @@ def test_conv_fast_variants_bit_identical(cfg, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_bn_act_and_backward(dtype):
+@pytest.mark.parametrize("C,N,H", [(64, 4, 9), (32, 2, 7), (192, 8, 33)])
+def test_bn_act_and_backward(dtype, C, N, H):
+    """BN finalize / apply / backward vs torch; every call is made twice and must
+    give identical results (no state carried between calls)."""
     from pose6d._lib import call, query, stream
     from pose6d.trunk import DTYPES
     g = torch.Generator().manual_seed(3)
-    N, H, W, C = 4, 9, 9, 64
+    W = H
     M = N * H * W
     y = torch.randn(N, C, H, W, generator=g) * 2 + 0.5
     res = torch.randn(N, C, H, W, generator=g)
@@ -196,14 +199,22 @@ def test_bn_act_and_backward(dtype):
     nbt = torch.zeros((), dtype=torch.long, device=dev)
     sc, sh, mu, iv = (torch.empty(C, device=dev) for _ in range(4))
     ws = torch.empty(64 * 3 * C, device=dev, dtype=torch.float64)
-    call("bn_finalize", stats, rows, C, M, gamma.to(dev), beta.to(dev), rm, rv, nbt, 0.1, 1e-5, 1, sc, sh, mu, iv, ws,
-         stream())
+    for rep in range(2):
+        if rep == 1:
+            first = [t.clone() for t in (sc, sh, mu, iv)]
+            rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+            nbt.zero_()
+        call("bn_finalize", stats, rows, C, M, gamma.to(dev), beta.to(dev), rm, rv, nbt, 0.1, 1e-5, 1, sc, sh, mu, iv,
+             ws, stream())
+    for a, b in zip(first, (sc, sh, mu, iv)):
+        assert torch.equal(a, b), "bn_finalize not repeatable"
     yd, rd = _nhwc(y).to(dev, dtype), _nhwc(res).to(dev, dtype)
     out = torch.empty_like(yd)
     call("bn_act_fwd", dt, yd, sc, sh, rd, None, None, 1, out, M, C, stream())
     yr = y.clone().requires_grad_(True)
+    gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
     rrm, rrv = torch.zeros(C), torch.ones(C)
-    o_ref = F.relu(F.batch_norm(yr, rrm, rrv, gamma, beta, True, 0.1, 1e-5) + res)
+    o_ref = F.relu(F.batch_norm(yr, rrm, rrv, gr, br, True, 0.1, 1e-5) + res)
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     _close(out.permute(0, 3, 1, 2), o_ref.detach(), tol * 10, "bn_act")
     _close(rm, rrm, 1e-5, "running_mean")
@@ -217,9 +228,16 @@ def test_bn_act_and_backward(dtype):
     dy = torch.empty_like(yd)
     dz = torch.empty_like(yd)
     dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
-    call("bn_bwd", dt, _nhwc(dout).to(dev, dtype), out, yd, mu, iv, gamma.to(dev), dg, db, 0, dy, dz, ws, M, C,
-         stream())
+    for rep in range(2):
+        call("bn_bwd", dt, _nhwc(dout).to(dev, dtype), out, yd, mu, iv, gamma.to(dev), dg, db, 0, dy, dz, ws, M, C,
+             stream())
+        if rep == 0:
+            first = [t.clone() for t in (dy, dg, db)]
+    for a, b in zip(first, (dy, dg, db)):
+        assert torch.equal(a, b), "bn_bwd not repeatable"
     _close(dy.permute(0, 3, 1, 2), yr.grad, 1e-4 if dtype == torch.float32 else 3e-2, "bn dy")
+    _close(dg, gr.grad, 1e-4 if dtype == torch.float32 else 3e-2, "dgamma")
+    _close(db, br.grad, 1e-4 if dtype == torch.float32 else 3e-2, "dbeta")
     mask = (o_ref.detach() > 0).float()
     _close(dz.permute(0, 3, 1, 2), dout * mask, 1e-6, "dz")
 
