@@ -22,6 +22,7 @@
 
 #include "common.h"
 #include "lds_dma.h"
+#include "wgrad_body.h"
 
 namespace {
 
@@ -382,21 +383,22 @@ __device__ __forceinline__ void lds_read_frags(u32x4 (&f)[NR], const unsigned (&
   }
 }
 
+// one workgroup's work; `bid_in` = its index in this conv's sub-grid (the whole grid,
+// or the leading part of a fused backward launch), `smem` = the kernel's dynamic LDS
 template <int BM, int BN, int MODE, int S>
-__global__ __launch_bounds__(kThreads) void conv_lds_kernel(const bf16* __restrict__ src, const bf16* __restrict__ wts,
-                                                            const float* __restrict__ bias,
-                                                            const bf16* __restrict__ res, bf16* __restrict__ out,
-                                                            float* __restrict__ stats, Geom g) {
+__device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16* __restrict__ src,
+                                              const bf16* __restrict__ wts, const float* __restrict__ bias,
+                                              const bf16* __restrict__ res, bf16* __restrict__ out,
+                                              float* __restrict__ stats, const Geom& g) {
   constexpr int TM = BM / 32, TN = BN / 32;
   constexpr int A_INS = BM / 32, B_INS = BN / 32;   // DMA instructions per thread per stage
   constexpr int LOADS = A_INS + B_INS;
   constexpr int SA = BM * 128, STAGE = (BM + BN) * 128;
   static_assert(S >= 2, "ring needs two stages");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int per = g.gm * g.gn;
   const int nwg = MODE == kDgradS2 ? 4 * per : per;
-  int bid = blockIdx.x;
+  int bid = bid_in;
   {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
@@ -554,6 +556,35 @@ __global__ __launch_bounds__(kThreads) void conv_lds_kernel(const bf16* __restri
   }
   asm volatile("s_barrier" ::: "memory");   // every wave done reading the ring before the epilogue reuses it
   conv_epilogue<bf16, BM, BN>(acc, smem, g, bias, res, out, stats, m0, n0, cls);
+}
+
+template <int BM, int BN, int MODE, int S>
+__global__ __launch_bounds__(kThreads) void conv_lds_kernel(const bf16* __restrict__ src, const bf16* __restrict__ wts,
+                                                            const float* __restrict__ bias,
+                                                            const bf16* __restrict__ res, bf16* __restrict__ out,
+                                                            float* __restrict__ stats, Geom g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  conv_lds_body<BM, BN, MODE, S>(smem, blockIdx.x, src, wts, bias, res, out, stats, g);
+}
+
+// Fused backward of one conv: workgroups [0, nd) compute the data gradient,
+// [nd_pad, nd_pad + nw) the weight gradient (nd_pad = nd rounded up to 8 keeps
+// each part's XCD remap intact; the padding workgroups exit at once).  Both read
+// the same dY, and the weight-gradient workgroups fill the CUs the (often small)
+// data-gradient grid leaves idle -- one launch instead of two.
+template <int DMODE, int DS, int WS>
+__global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ wt,
+                                                            const bf16* __restrict__ dres, bf16* __restrict__ dx,
+                                                            Geom gd, int nd, int nd_pad,
+                                                            const bf16* __restrict__ x, float* __restrict__ ws,
+                                                            p6::WGeom gw) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int b = blockIdx.x;
+  if (b < nd_pad) {
+    if (b < nd) conv_lds_body<64, 64, DMODE, DS>(smem, b, dy, wt, nullptr, dres, dx, nullptr, gd);
+  } else {
+    conv_wgrad_lds_body<64, 64, WS>(smem, b - nd_pad, x, dy, ws, gw);
+  }
 }
 
 // K-steps of the longest work item (kDgradS2: the class with the most taps)
@@ -813,6 +844,84 @@ extern "C" int pose6d_conv2d_dgrad(int32_t dtype, const void* dy, const void* wt
   const Geom g = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
   P6_CHECK_ARG(g.log2SC >= 0 && Cout % bk == 0, "pose6d_conv2d_dgrad: Cout must be a power of two >= %d", bk);
   return run_conv(dtype, mode, g, dy, wt, nullptr, dres, dx, nullptr, p6::stream_of(stream));
+}
+
+namespace {
+
+template <int DMODE, int DS, int WS>
+int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void* wt, const void* dres, void* dx,
+               const void* x, float* ws, hipStream_t s) {
+  Geom gd = gd0;
+  gd.gm = p6::ceil_div(gd.M, 64);
+  gd.gn = p6::ceil_div(gd.Ncols, 64);
+  const int nd = gd.gm * gd.gn * (DMODE == kDgradS2 ? 4 : 1);
+  const int nd_pad = (nd + 7) & ~7;
+  const int nw = gw.gm * gw.gn * gw.splits;
+  const int nk = fast_nk(DMODE, gd);
+  const int ring_d = (nk < DS ? (nk > 0 ? nk : 1) : DS) * 128 * 128;
+  const int epi = 64 * (64 * 2 + 16);
+  const int ring_w = WS * 128 * 128;
+  int lds = ring_d > epi ? ring_d : epi;
+  lds = lds > ring_w ? lds : ring_w;
+  conv_bwd_kernel<DMODE, DS, WS><<<nd_pad + nw, kThreads, lds, s>>>((const bf16*)dy, (const bf16*)wt,
+                                                                    (const bf16*)dres, (bf16*)dx, gd, nd, nd_pad,
+                                                                    (const bf16*)x, ws, gw);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+template <int DMODE>
+int launch_bwd_mode(int ds, const Geom& gd, const p6::WGeom& gw, const void* dy, const void* wt, const void* dres,
+                    void* dx, const void* x, float* ws, hipStream_t s) {
+  return ds == 2 ? launch_bwd<DMODE, 2, 3>(gd, gw, dy, wt, dres, dx, x, ws, s)
+                 : launch_bwd<DMODE, 4, 3>(gd, gw, dy, wt, dres, dx, x, ws, s);
+}
+
+}  // namespace
+
+// Data + weight gradient of one conv.  When both passes take the bf16 LDS-DMA
+// kernels (64x64 tiles, data-gradient ring of 2 or 4 slots, weight-gradient ring
+// of 3) they run as ONE launch of conv_bwd_kernel, followed by the slab reduce;
+// otherwise as the separate pose6d_conv2d_dgrad + pose6d_conv2d_wgrad launches.
+// dx == NULL: weight gradient only.
+extern "C" int pose6d_conv2d_backward(int32_t dtype, const void* x, const void* dy, const void* wt, const void* dres,
+                                      void* dx, float* dw, int32_t accumulate, float* workspace, int64_t ws_bytes,
+                                      int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout,
+                                      int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
+                                      void* stream) {
+  P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_backward: bad dtype %d", dtype);
+  if (dx == nullptr)
+    return pose6d_conv2d_wgrad(dtype, x, dy, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real, Cout, KH,
+                               KW, stride, pad, Ho, Wo, stream);
+  P6_CHECK_ARG(stride == 1 || stride == 2, "pose6d_conv2d_backward: stride must be 1 or 2");
+  P6_CHECK_ARG(Cin % 8 == 0 && Cin_real <= Cin && ilog2(Cin) >= 3,
+               "pose6d_conv2d_backward: Cin must be a power of two >= 8 for the data gradient");
+  int mode;
+  const Geom gd0 = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
+  const Plan pd = choose(dtype, mode, gd0);
+  p6::WgradPlan pw;
+  const p6::WGeom gw = p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
+  const bool fused = pd.fast && pd.tile == 3 && (pd.stages == 2 || pd.stages == 4) && pw.fast && pw.stages == 3 &&
+                     getenv("POSE6D_BWD_SEPARATE") == nullptr;
+  if (!fused) {
+    const int rc = pose6d_conv2d_dgrad(dtype, dy, wt, dres, dx, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo,
+                                       stream);
+    if (rc) return rc;
+    return pose6d_conv2d_wgrad(dtype, x, dy, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real, Cout, KH,
+                               KW, stride, pad, Ho, Wo, stream);
+  }
+  P6_CHECK_ARG((int64_t)pw.splits * Cout * gw.Kpad * 4 <= ws_bytes,
+               "pose6d_conv2d_backward: workspace %lld bytes < %lld needed", (long long)ws_bytes,
+               (long long)pw.splits * Cout * gw.Kpad * 4);
+  hipStream_t s = p6::stream_of(stream);
+  int rc;
+  switch (pd.mode) {
+    case kGemm: rc = launch_bwd_mode<kGemm>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, s); break;
+    case kDgradS2: rc = launch_bwd_mode<kDgradS2>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, s); break;
+    default: rc = launch_bwd_mode<kDgrad>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, s); break;
+  }
+  if (rc) return rc;
+  return p6::wgrad_reduce_launch(workspace, dw, Cout, gw.Kpad, Cin, Cin_real, KH, KW, gw.splits, accumulate, s);
 }
 
 // launch variant of a forward / data-gradient conv, for profiling joins:

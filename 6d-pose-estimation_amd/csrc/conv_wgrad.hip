@@ -15,9 +15,11 @@
 
 #include "common.h"
 #include "lds_dma.h"
+#include "wgrad_body.h"
 
 namespace {
 
+using p6::WGeom;
 constexpr int kThreads = 256;
 constexpr int MT = 32;  // m rows per reduction step
 
@@ -25,13 +27,6 @@ template <typename T> struct WT;
 template <> struct WT<bf16> { static constexpr int VEC = 8; };
 template <> struct WT<float> { static constexpr int VEC = 4; };
 
-struct WGeom {
-  int M, Cout, K, Kpad;
-  int SH, SW, SC, log2SC;
-  int RH, RW;
-  int KH, KW, stride, pad;
-  int gm, gn, splits, mps;  // tiles over Cout, over K; splits; m per split (multiple of MT)
-};
 
 // XOR (in 16-B chunk units, always even: keeps 32-B pairs together) for a row of
 // `pairs` 32-byte pairs, such that rows {0..3, 8..11} (and {4..7, 12..15}) of a
@@ -228,199 +223,6 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const T* __restric
 }
 
 
-// ============================================================================
-// Fast path (bf16, Cin a multiple of 64, Cout a multiple of 64): each stage is
-// 64 pixels deep; dY [64 m][64 co] and X [64 m][64 k] sub-images (one filter tap,
-// 64 contiguous channels per X row) are filled by LDS-DMA (8 rows x 128 B per
-// wave instruction, XOR swizzle on the source chunk) through an S-slot ring with
-// counted vmcnt + raw barriers, and read back transposed with ds_read_b64_tr_b16
-// in one asm block per k-half (see lds_read_frags in conv_igemm.hip for why the
-// reads are asm).  Rows past the split's end read the zero page.
-// ============================================================================
-__device__ __forceinline__ int swz_tr4(int r) { return ((((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1); }
-
-typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
-
-// 2 * NF transposed reads (NF operands of 8 m each) + lgkmcnt(0), as one asm block
-template <int NF>
-__device__ __forceinline__ void lds_read_tr_frags(u32x2 (&f)[2 * NF], const unsigned (&a)[2 * NF]) {
-  static_assert(NF == 2 || NF == 4, "2 or 4 operands per batch");
-  if constexpr (NF == 2) {
-    asm volatile(
-        "ds_read_b64_tr_b16 %0, %4\n\tds_read_b64_tr_b16 %1, %5\n\tds_read_b64_tr_b16 %2, %6\n\t"
-        "ds_read_b64_tr_b16 %3, %7\n\ts_waitcnt lgkmcnt(0)"
-        : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3])
-        : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]));
-  } else {
-    asm volatile(
-        "ds_read_b64_tr_b16 %0, %8\n\tds_read_b64_tr_b16 %1, %9\n\tds_read_b64_tr_b16 %2, %10\n\t"
-        "ds_read_b64_tr_b16 %3, %11\n\tds_read_b64_tr_b16 %4, %12\n\tds_read_b64_tr_b16 %5, %13\n\t"
-        "ds_read_b64_tr_b16 %6, %14\n\tds_read_b64_tr_b16 %7, %15\n\ts_waitcnt lgkmcnt(0)"
-        : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]), "=&v"(f[4]), "=&v"(f[5]), "=&v"(f[6]), "=&v"(f[7])
-        : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]));
-  }
-}
-
-template <int BM, int BN, int S>
-__global__ __launch_bounds__(kThreads) void conv_wgrad_lds_kernel(const bf16* __restrict__ x,
-                                                                  const bf16* __restrict__ dy,
-                                                                  float* __restrict__ ws, WGeom g) {
-  constexpr int MS = 64;                          // pixels per stage
-  constexpr int YS = BM / 64, XS = BN / 64;       // 64-column sub-images per operand
-  constexpr int LOADS = 2 * (YS + XS);            // DMA instructions per thread per stage
-  constexpr int SUB = MS * 128;                   // bytes per sub-image
-  constexpr int STAGE = (YS + XS) * SUB;
-  constexpr int TM = BM / 32, TN = BN / 32;
-  static_assert((TM + TN) % 2 == 0 && TM + TN <= 8, "fragment batches of 2 or 4 operands");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int tiles = g.gm * g.gn;
-  const int nwg = tiles * g.splits;
-  int bid = blockIdx.x;
-  {
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  }
-  const int split = bid / tiles;   // all tiles of one pixel range share an XCD's L2
-  const int t2 = bid - split * tiles;
-  const int tm = t2 / g.gn, tn = t2 - tm * g.gn;
-  const int co0 = tm * BM, k0 = tn * BN;
-  const int mbeg = split * g.mps;
-  const int mend = min(g.M, mbeg + g.mps);
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int r8 = lane >> 3, pch = lane & 7;
-  const char* zp = reinterpret_cast<const char*>(g_zero_page);
-  const bool pointwise = g.KH == 1 && g.KW == 1 && g.stride == 1 && g.pad == 0;
-
-  // each thread DMAs rows R = i * 32 + wave * 8 + r8 (i = 0, 1) of every sub-image;
-  // the logical chunk it fetches carries the row's swizzle
-  int ck[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) ck[i] = (pch ^ swz_tr4(i * 32 + wave * 8 + r8)) * 8;
-  int tap_h[XS], tap_w[XS], ci0[XS];
-#pragma unroll
-  for (int s = 0; s < XS; ++s) {
-    const int kk0 = k0 + s * 64;
-    const int tap = kk0 >> g.log2SC;
-    ci0[s] = kk0 & (g.SC - 1);
-    tap_h[s] = tap / g.KW;
-    tap_w[s] = tap - tap_h[s] * g.KW;
-  }
-  const int hw = g.RH * g.RW;
-
-  auto issue = [&](int st, int buf) {
-    char* base = smem + buf * STAGE;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int R = i * 32 + wave * 8 + r8;
-      const int m = mbeg + st * MS + R;
-      const bool ok = m < mend;
-#pragma unroll
-      for (int s = 0; s < YS; ++s) {
-        const void* p = ok ? (const void*)(dy + (int64_t)m * g.Cout + co0 + s * 64 + ck[i]) : (const void*)zp;
-        glds16(p, base + s * SUB + (i * 32 + wave * 8) * 128);
-      }
-      int n = 0, sy = 0, sx = 0;
-      if (!pointwise) {
-        const int mm = ok ? m : 0;
-        n = mm / hw;
-        const int rem = mm - n * hw;
-        const int oy = rem / g.RW;
-        sy = oy * g.stride - g.pad;
-        sx = (rem - oy * g.RW) * g.stride - g.pad;
-      }
-#pragma unroll
-      for (int s = 0; s < XS; ++s) {
-        const void* p = zp;
-        if (pointwise) {
-          if (ok) p = x + ((int64_t)m << g.log2SC) + ci0[s] + ck[i];
-        } else {
-          const int yy = sy + tap_h[s], xx = sx + tap_w[s];
-          if (ok && (unsigned)yy < (unsigned)g.SH && (unsigned)xx < (unsigned)g.SW)
-            p = x + ((((int64_t)n * g.SH + yy) * g.SW + xx) << g.log2SC) + ci0[s] + ck[i];
-        }
-        glds16(p, base + (YS + s) * SUB + (i * 32 + wave * 8) * 128);
-      }
-    }
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // transposed-read byte offsets in a slot: operand o, half h, k-half kk
-  const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  unsigned off[2][2 * (TM + TN)];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-    for (int o = 0; o < TM + TN; ++o)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const bool isy = o < TM;
-        const int col = isy ? wm * (BM / 2) + o * 16 + 4 * p : wn * (BN / 2) + (o - TM) * 16 + 4 * p;
-        const int sub = (isy ? 0 : YS) + (col >> 6), lc = col & 63;
-        const int r = 32 * kk + 8 * grp + 4 * h + q;
-        off[kk][2 * o + h] = sub * SUB + r * 128 + (((lc >> 3) ^ swz_tr4(r)) << 4) + (lc & 7) * 2;
-      }
-  const unsigned ring = lds_addr(smem);
-  auto compute = [&](int buf) {
-    const unsigned slot = ring + buf * STAGE;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      u32x2 f[2 * (TM + TN)];
-      constexpr int NB = TM + TN >= 4 ? 4 : 2;   // operands per asm batch
-#pragma unroll
-      for (int b0 = 0; b0 < TM + TN; b0 += NB) {
-        unsigned a[2 * NB];
-        u32x2 t[2 * NB];
-#pragma unroll
-        for (int u = 0; u < 2 * NB; ++u) a[u] = slot + off[kk][2 * b0 + u];
-        if constexpr (NB == 4) lds_read_tr_frags<4>(t, a);
-        else lds_read_tr_frags<2>(t, a);
-#pragma unroll
-        for (int u = 0; u < 2 * NB; ++u) f[2 * b0 + u] = t[u];
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const u32x4 av = {f[2 * i].x, f[2 * i].y, f[2 * i + 1].x, f[2 * i + 1].y};
-          const u32x4 bv = {f[2 * (TM + j)].x, f[2 * (TM + j)].y, f[2 * (TM + j) + 1].x, f[2 * (TM + j) + 1].y};
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av),
-                                                              __builtin_bit_cast(bf16x8, bv), acc[i][j], 0, 0, 0);
-        }
-    }
-  };
-
-  const int nk = (mend - mbeg + MS - 1) / MS;
-  for (int s = 0; s < S - 1 && s < nk; ++s) issue(s, s);
-  int cur = 0, wbuf = S - 1;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int left = nk - 1 - kt;
-    wait_ahead<LOADS, S - 2>(left < S - 2 ? left : S - 2);
-    if (kt + S - 1 < nk) issue(kt + S - 1, wbuf);
-    compute(cur);
-    cur = cur == S - 1 ? 0 : cur + 1;
-    wbuf = wbuf == S - 1 ? 0 : wbuf + 1;
-  }
-
-  float* slab = ws + (int64_t)split * g.Cout * g.Kpad;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wm * (BM / 2) + i * 16 + grp * 4 + r;
-        const int k = k0 + wn * (BN / 2) + j * 16 + li;
-        slab[(int64_t)co * g.Kpad + k] = acc[i][j][r];
-      }
-}
-
 // sum the split slabs (fixed order) into the OIHW fp32 gradient; k = (kh, kw, ci).
 // Block = L float4 lanes (4 consecutive k each) x G split groups: group g sums
 // slabs g, g + G, ... with U loads in flight, then the G partials are combined in
@@ -495,10 +297,15 @@ int launch_reduce(const float* ws, float* dw, int Cout, int Kpad, int SC, int Ci
   return POSE6D_OK;
 }
 
-struct Plan {
-  bool fast;
-  int bm, bn, splits, mps, stages;
-};
+using Plan = p6::WgradPlan;
+
+template <int S>
+__global__ __launch_bounds__(kThreads) void conv_wgrad_lds_kernel(const bf16* __restrict__ x,
+                                                                  const bf16* __restrict__ dy,
+                                                                  float* __restrict__ ws, WGeom g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  conv_wgrad_lds_body<64, 64, S>(smem, blockIdx.x, x, dy, ws, g);
+}
 
 int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
@@ -553,8 +360,7 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC) {
 template <int S>
 int launch_fast(const WGeom& g, const void* x, const void* dy, float* ws, hipStream_t s) {
   const int lds = S * (64 + 64) * 128;
-  conv_wgrad_lds_kernel<64, 64, S><<<g.gm * g.gn * g.splits, kThreads, lds, s>>>((const bf16*)x, (const bf16*)dy,
-                                                                                 ws, g);
+  conv_wgrad_lds_kernel<S><<<g.gm * g.gn * g.splits, kThreads, lds, s>>>((const bf16*)x, (const bf16*)dy, ws, g);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
@@ -592,22 +398,38 @@ extern "C" int64_t pose6d_conv2d_wgrad_workspace(int32_t dtype, int32_t N, int32
   return (int64_t)p.splits * Cout * Kpad * 4;
 }
 
-extern "C" int pose6d_conv2d_wgrad(int32_t dtype, const void* x, const void* dy, float* dw, int32_t accumulate,
-                                   float* workspace, int64_t ws_bytes, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cin_real,
-                                   int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho,
-                                   int32_t Wo, void* stream) {
-  P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_wgrad: bad dtype %d", dtype);
-  const int lc = ilog2(Cin);
-  P6_CHECK_ARG(lc >= 2 && Cout % 8 == 0 && Cin_real <= Cin, "pose6d_conv2d_wgrad: Cin must be a power of two >= 4");
+namespace p6 {
+
+WGeom wgrad_geom(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad, int Ho,
+                 int Wo, WgradPlan* plan_out) {
   const int bk = dtype == POSE6D_DT_BF16 ? 32 : 16;
-  P6_CHECK_ARG(dtype == POSE6D_DT_BF16 || Cin % 4 == 0, "pose6d_conv2d_wgrad: bad Cin");
   WGeom g{};
-  g.M = N * Ho * Wo; g.Cout = Cout; g.K = KH * KW * Cin; g.Kpad = p6::ceil_div(g.K, bk) * bk;
-  g.SH = H; g.SW = W; g.SC = Cin; g.log2SC = lc; g.RH = Ho; g.RW = Wo;
+  g.M = N * Ho * Wo; g.Cout = Cout; g.K = KH * KW * Cin; g.Kpad = ceil_div(g.K, bk) * bk;
+  g.SH = H; g.SW = W; g.SC = Cin; g.log2SC = ilog2(Cin); g.RH = Ho; g.RW = Wo;
   g.KH = KH; g.KW = KW; g.stride = stride; g.pad = pad;
   const Plan p = plan(dtype, g.M, Cout, g.Kpad, Cin);
-  g.gm = p6::ceil_div(Cout, p.bm); g.gn = p6::ceil_div(g.Kpad, p.bn);
+  g.gm = ceil_div(Cout, p.bm); g.gn = ceil_div(g.Kpad, p.bn);
   g.splits = p.splits; g.mps = p.mps;
+  if (plan_out) *plan_out = p;
+  return g;
+}
+
+int wgrad_reduce_launch(const float* ws, float* dw, int Cout, int Kpad, int SC, int Cin, int KH, int KW, int splits,
+                        int accumulate, hipStream_t s) {
+  return launch_reduce(ws, dw, Cout, Kpad, SC, Cin, KH, KW, splits, accumulate, s);
+}
+
+}  // namespace p6
+
+extern "C" int pose6d_conv2d_wgrad(int32_t dtype, const void* x, const void* dy, float* dw, int32_t accumulate,
+                                   float* workspace, int64_t ws_bytes, int32_t N, int32_t H, int32_t W, int32_t Cin,
+                                   int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
+                                   int32_t pad, int32_t Ho, int32_t Wo, void* stream) {
+  P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_wgrad: bad dtype %d", dtype);
+  P6_CHECK_ARG(ilog2(Cin) >= 2 && Cout % 8 == 0 && Cin_real <= Cin,
+               "pose6d_conv2d_wgrad: Cin must be a power of two >= 4");
+  Plan p;
+  const WGeom g = p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &p);
   P6_CHECK_ARG((int64_t)p.splits * Cout * g.Kpad * 4 <= ws_bytes,
                "pose6d_conv2d_wgrad: workspace %lld bytes < %lld needed (query pose6d_conv2d_wgrad_workspace with the "
                "same environment)", (long long)ws_bytes, (long long)p.splits * Cout * g.Kpad * 4);

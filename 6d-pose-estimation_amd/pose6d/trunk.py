@@ -17,8 +17,6 @@ differentiates (checked with a generation counter).
 """
 import ctypes
 
-import os
-
 import numpy as np
 import torch
 import torch.nn as nn
@@ -286,8 +284,6 @@ class TrunkEngine:
         if self._saved_gen != self.generation:
             raise Pose6dError("TrunkEngine.backward: activations of the matching training forward were overwritten")
         st = stream()
-        main = torch.cuda.current_stream()
-        side = self._side_stream() if os.environ.get("POSE6D_WGRAD_SIDE", "0") == "1" else main
         dt = self.dt
         B = self.B
         acc = int(accumulate)
@@ -315,47 +311,31 @@ class TrunkEngine:
             elif isinstance(op, _ConvOp):
                 dy = op.out.g
                 M = B * op.Ho * op.Wo
-                # the weight gradient is off the critical path: it runs on the side
-                # stream (its own workspace, in order there) beside the data gradient
-                if side is not main:
-                    ev = torch.cuda.Event()
-                    ev.record(main)
-                    side.wait_event(ev)
-                with torch.cuda.stream(side):
-                    sst = stream()
-                    call("conv2d_wgrad", dt, op.src.t, dy, grad_of(op.conv.weight), acc, self.ws_wgrad,
-                         self.ws_wgrad.numel() * 4, B, op.H, op.W, op.cin_pad, op.cin, op.cout, op.k, op.k,
-                         op.stride, op.pad, op.Ho, op.Wo, sst)
-                    if op.conv.bias is not None:
-                        call("channel_sum", dt, dy, M, op.cout, grad_of(op.conv.bias), acc, sst)
-                    if on_conv_done is not None:
-                        on_conv_done(op)   # records its event on the side stream
+                dres, dx = None, None
                 if op.needs_dgrad:
                     src = op.src
                     if src.pending is not None and src.g is not None and src.pending is not src.g:
                         # a residual contribution is waiting: fuse it into this dgrad's epilogue
-                        call("conv2d_dgrad", dt, dy, op.wt, src.pending, src.g, B, op.H, op.W, op.cin_pad, op.cout,
-                             op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, st)
+                        dres, dx = src.pending, src.g
                         src.pending = None
                     elif src.pending is None and self._has_later_consumer(op):
-                        # first of two contributions (downsample branch): park it in dres
-                        call("conv2d_dgrad", dt, dy, op.wt, None, op.dres, B, op.H, op.W, op.cin_pad, op.cout, op.k,
-                             op.k, op.stride, op.pad, op.Ho, op.Wo, st)
+                        # first of two contributions (downsample branch): park it in op.dres
+                        dx = op.dres
                         src.pending = op.dres
                     else:
-                        call("conv2d_dgrad", dt, dy, op.wt, None, src.g, B, op.H, op.W, op.cin_pad, op.cout, op.k,
-                             op.k, op.stride, op.pad, op.Ho, op.Wo, st)
+                        dx = src.g
+                # data + weight gradient: one fused launch on the bf16 fast path
+                call("conv2d_backward", dt, op.src.t, dy, op.wt, dres, dx, grad_of(op.conv.weight), acc,
+                     self.ws_wgrad, self.ws_wgrad.numel() * 4, B, op.H, op.W, op.cin_pad, op.cin, op.cout, op.k,
+                     op.k, op.stride, op.pad, op.Ho, op.Wo, st)
+                if op.conv.bias is not None:
+                    call("channel_sum", dt, dy, M, op.cout, grad_of(op.conv.bias), acc, st)
+                if on_conv_done is not None:
+                    on_conv_done(op)
             else:
                 s = op.src
                 call("maxpool_bwd", dt, op.out.g, op.argmax, s.g, B, s.H, s.W, s.C, op.k, op.s, op.p, op.out.H,
                      op.out.W, st)
-        if side is not main:
-            main.wait_stream(side)   # every weight gradient is final when backward returns
-
-    def _side_stream(self):
-        if getattr(self, "_side", None) is None or self._side.device != torch.cuda.current_stream().device:
-            self._side = torch.cuda.Stream(device=torch.cuda.current_stream().device)
-        return self._side
 
     def _has_later_consumer(self, op):
         """True if op.src is also consumed by a conv processed later in backward

@@ -159,6 +159,15 @@ int pose6d_conv2d_wgrad(int32_t dtype, const void *x, const void *dy, float *dw,
                         int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
                         void *stream);
 
+/* Data + weight gradient of one conv in one call (pose6d_conv2d_dgrad followed by
+ * pose6d_conv2d_wgrad, same arguments and workspace): on the bf16 LDS-DMA paths
+ * both run as ONE launch whose workgroups split between the two passes, then
+ * the slab reduce.  dx == NULL skips the data gradient. */
+int pose6d_conv2d_backward(int32_t dtype, const void *x, const void *dy, const void *wt, const void *dres,
+                           void *dx, float *dw, int32_t accumulate, float *workspace, int64_t ws_bytes, int32_t N,
+                           int32_t H, int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH,
+                           int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, void *stream);
+
 /* nn.BatchNorm2d: finalize the conv-epilogue statistics (training) or use the
  * running statistics (eval) -> scale/shift (+ saved mean / invstd); running
  * stats, num_batches_tracked updated in training (torch semantics).

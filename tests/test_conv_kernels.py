@@ -160,6 +160,20 @@ def test_conv_fast_variants_bit_identical(cfg, monkeypatch):
         assert torch.equal(y0, y1), f"fwd differs under {env}"
         assert torch.equal(dx0, dx1), f"dgrad differs under {env}"
         assert torch.equal(dw0, dw1), f"wgrad differs under {env}"
+    # the fused data+weight gradient launch must equal the two separate passes bit for bit
+    for key in keys:
+        monkeypatch.delenv(key, raising=False)
+    for sep in (False, True):
+        if sep:
+            monkeypatch.setenv("POSE6D_BWD_SEPARATE", "1")
+        dxf = torch.empty(N, H, W, Cin, device=dev, dtype=dtype)
+        dwf = torch.empty(Cout, Cin, k, k, device=dev)
+        call("conv2d_backward", dt, x, dy, wt, dres, dxf, dwf, 0, ws, ws.numel() * 4, N, H, W, Cin, Cin, Cout, k, k,
+             s, p, Ho, Wo, stream())
+        torch.cuda.synchronize()
+        assert torch.equal(dxf.cpu(), dx0), f"fused backward dx differs (separate={sep})"
+        assert torch.equal(dwf.cpu(), dw0), f"fused backward dw differs (separate={sep})"
+    monkeypatch.delenv("POSE6D_BWD_SEPARATE", raising=False)
     # the register-staged weight gradient sums the pixels in other splits: close, not equal
     for key in keys:
         monkeypatch.delenv(key, raising=False)
