@@ -12,6 +12,8 @@
 // pose6d_bn_bwd_finalize -> dgamma/dbeta + coefficients, pose6d_bn_bwd_apply ->
 // dy = gamma*invstd*(dz - mean(dz) - xhat*mean(dz*xhat)), optionally emitting dz
 // (the gradient of a residual identity branch).
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -90,6 +92,84 @@ __global__ __launch_bounds__(kThreads) void bn_stats_stage1_kernel(const float* 
     ws[((int64_t)s * 3 + 0) * C + c] = w.n;
     ws[((int64_t)s * 3 + 1) * C + c] = w.mean;
     ws[((int64_t)s * 3 + 2) * C + c] = w.m2;
+  }
+}
+
+// ONE launch (training): block = 256 / L channels x L lanes (L = 64 or 256 by the
+// row count); lane l folds partial rows l, l + L, ... of its channel as shifted
+// sums about K = row 0's mean:
+//   S1 = sum_i (sum_i - n_i K),  S2 = sum_i (M2_i + n_i (mean_i - K)^2)
+// (fp64, no divisions: n_i = 32 except the last row), the lanes combine by a
+// fixed xor-shuffle tree (+ an LDS step across waves for L = 256:
+// deterministic), and mean = K + S1/N, var = (S2 - S1^2/N)/N.  The shift keeps
+// S1^2/N small against S2 (K is a mean of the same data): no E[x^2]-E[x]^2
+// cancellation.
+template <int L>
+__global__ __launch_bounds__(kThreads) void bn_stats_finalize_kernel(
+    const float* __restrict__ part, int rows, int C, int64_t M, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
+    float momentum, float eps, float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ smean,
+    float* __restrict__ sinv) {
+  __shared__ double red[2][kThreads / 64];
+  const int lane = threadIdx.x % L;
+  const int c = blockIdx.x * (kThreads / L) + threadIdx.x / L;
+  double s1 = 0.0, s2 = 0.0, K = 0.0;
+  if (c < C) {
+    K = (double)part[c] / (double)min((int64_t)32, M);
+    const double n_last = (double)(M - (int64_t)(rows - 1) * 32), inv_last = 1.0 / n_last;
+    constexpr int U = 4;
+    int r = lane;
+    for (; r + (U - 1) * L < rows; r += U * L) {
+      float sv[U], qv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        sv[u] = part[(int64_t)(r + u * L) * 2 * C + c];
+        qv[u] = part[(int64_t)(r + u * L) * 2 * C + C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool last = r + u * L == rows - 1;
+        const double n = last ? n_last : 32.0, inv_n = last ? inv_last : 0.03125;
+        const double d = (double)sv[u] - n * K;        // n_i (mean_i - K)
+        s1 += d;
+        s2 += (double)qv[u] + d * d * inv_n;
+      }
+    }
+    for (; r < rows; r += L) {
+      const bool last = r == rows - 1;
+      const double n = last ? n_last : 32.0, inv_n = last ? inv_last : 0.03125;
+      const double d = (double)part[(int64_t)r * 2 * C + c] - n * K;
+      s1 += d;
+      s2 += (double)part[(int64_t)r * 2 * C + C + c] + d * d * inv_n;
+    }
+  }
+  s1 = p6::wave_sum(s1);
+  s2 = p6::wave_sum(s2);
+  if constexpr (L > 64) {
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[0][w] = s1; red[1][w] = s2; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      s1 = 0.0; s2 = 0.0;
+#pragma unroll
+      for (int i = 0; i < kThreads / 64; ++i) { s1 += red[0][i]; s2 += red[1][i]; }
+    }
+  }
+  if (lane == 0 && c < C) {
+    const double N = (double)M;
+    const double mean = K + s1 / N;
+    double var = (s2 - s1 * s1 / N) / N;
+    if (var < 0.0) var = 0.0;
+    const float inv = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = gamma[c] * inv;
+    scale[c] = sc;
+    shift[c] = beta[c] - (float)mean * sc;
+    smean[c] = (float)mean;
+    sinv[c] = inv;
+    const double unb = N > 1.0 ? var * N / (N - 1.0) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+    if (c == 0 && nbt) nbt[0] += 1;
   }
 }
 
@@ -378,6 +458,19 @@ extern "C" int pose6d_bn_finalize(const float* partial, int32_t rows, int32_t C,
   P6_CHECK_ARG(C > 0 && (!training || (rows > 0 && count > 0 && workspace)), "pose6d_bn_finalize: bad sizes");
   hipStream_t s = p6::stream_of(stream);
   int splits = 0;
+  if (training && getenv("POSE6D_BN_TWO_STAGE") == nullptr) {
+    if (rows > 512)
+      bn_stats_finalize_kernel<256><<<C, kThreads, 0, s>>>(partial, rows, C, count, gamma, beta, running_mean,
+                                                            running_var, num_batches, momentum, eps, scale, shift,
+                                                            save_mean, save_invstd);
+    else
+      bn_stats_finalize_kernel<64><<<p6::ceil_div(C, 4), kThreads, 0, s>>>(partial, rows, C, count, gamma, beta,
+                                                                          running_mean, running_var, num_batches,
+                                                                          momentum, eps, scale, shift, save_mean,
+                                                                          save_invstd);
+    P6_LAUNCH_CHECK();
+    return POSE6D_OK;
+  }
   if (training) {
     splits = rows < kSplits ? rows : kSplits;
     bn_stats_stage1_kernel<<<dim3(p6::ceil_div(C, 16), splits), kThreads, 0, s>>>(partial, rows, C, count, workspace);

@@ -172,8 +172,9 @@ int pose6d_conv2d_backward(int32_t dtype, const void *x, const void *dy, const v
  * running statistics (eval) -> scale/shift (+ saved mean / invstd); running
  * stats, num_batches_tracked updated in training (torch semantics).
  * partial: `rows` = ceil(count / 32) rows of [2][C] (sum, M2 about the row's mean)
- * over 32-pixel blocks; merged with Chan's parallel-variance formula in fp64
- * (two launches); workspace: 64 * 3 * C doubles. */
+ * over 32-pixel blocks, folded in fp64 as shifted sums about the first row's
+ * mean in ONE launch (env POSE6D_BN_TWO_STAGE: the earlier two-launch Chan
+ * merge); workspace: 64 * 3 * C doubles (used by the two-stage form only). */
 int pose6d_bn_finalize(const float *partial, int32_t rows, int32_t C, int64_t count, const float *gamma,
                        const float *beta, float *running_mean, float *running_var, int64_t *num_batches,
                        float momentum, float eps, int32_t training, float *scale, float *shift, float *save_mean,
