@@ -14,6 +14,8 @@
 // (the gradient of a residual identity branch).
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -265,8 +267,31 @@ __global__ __launch_bounds__(kThreads) void bn_act_kernel(const T* __restrict__ 
 // ---------------------------------------------------------------- backward
 // grid (channel-chunk groups, row blocks): block = CL chunk-lanes (consecutive 16-B
 // chunks of a row: coalesced) x RL row-lanes; partial row = blockIdx.y.
-template <typename T, bool HAS_OUT>
+// ReLU mask of the forward output: MK 0 none, 1 out > 0 (read), 2 recomputed from
+// the raw conv output y as bf16-or-fp32(y * scale + shift) > 0 -- exactly the sign
+// pose6d_bn_act_fwd stored, without reading its output (no residual on that BN)
+template <int MK, typename T>
+__device__ __forceinline__ void relu_mask(float (&d)[V<T>::E], const uint4& ov, const float (&yy)[V<T>::E],
+                                          const float* __restrict__ rs, const float* __restrict__ rb, int c0) {
+  constexpr int E = V<T>::E;
+  if constexpr (MK == 1) {
+    float o[E];
+    load_vec(reinterpret_cast<const T*>(&ov), o);
+#pragma unroll
+    for (int e = 0; e < E; ++e) d[e] = o[e] > 0.f ? d[e] : 0.f;
+  } else if constexpr (MK == 2) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float v = p6::to_f(p6::from_f<T>(fmaf(yy[e], rs[c0 + e], rb[c0 + e])));
+      d[e] = v > 0.f ? d[e] : 0.f;
+    }
+  }
+}
+
+template <typename T, int MK>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce2_kernel(const T* __restrict__ dout, const T* __restrict__ out,
+                                                                  const float* __restrict__ rs,
+                                                                  const float* __restrict__ rb,
                                                                   const T* __restrict__ y,
                                                                   const float* __restrict__ mean,
                                                                   const float* __restrict__ inv,
@@ -294,20 +319,15 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce2_kernel(const T* __res
     for (int u = 0; u < U; ++u) {
       const int64_t off = (r + u * RL) * C + c0;
       dv[u] = *reinterpret_cast<const uint4*>(dout + off);
-      if constexpr (HAS_OUT) ov[u] = *reinterpret_cast<const uint4*>(out + off);
+      if constexpr (MK == 1) ov[u] = *reinterpret_cast<const uint4*>(out + off);
       yv[u] = *reinterpret_cast<const uint4*>(y + off);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       float d[E], yy[E];
       load_vec(reinterpret_cast<const T*>(&dv[u]), d);
-      if constexpr (HAS_OUT) {
-        float o[E];
-        load_vec(reinterpret_cast<const T*>(&ov[u]), o);
-#pragma unroll
-        for (int e = 0; e < E; ++e) d[e] = o[e] > 0.f ? d[e] : 0.f;
-      }
       load_vec(reinterpret_cast<const T*>(&yv[u]), yy);
+      relu_mask<MK, T>(d, ov[u], yy, rs, rb, c0);
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         s[e] += d[e];
@@ -318,14 +338,11 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce2_kernel(const T* __res
   for (; r < r1; r += RL) {
     const int64_t off = r * C + c0;
     float d[E], yy[E];
+    uint4 ov{};
     load_vec(dout + off, d);
-    if constexpr (HAS_OUT) {
-      float o[E];
-      load_vec(out + off, o);
-#pragma unroll
-      for (int e = 0; e < E; ++e) d[e] = o[e] > 0.f ? d[e] : 0.f;
-    }
+    if constexpr (MK == 1) ov = *reinterpret_cast<const uint4*>(out + off);
     load_vec(y + off, yy);
+    relu_mask<MK, T>(d, ov, yy, rs, rb, c0);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       s[e] += d[e];
@@ -385,8 +402,10 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_finalize_kernel(const float* 
   }
 }
 
-template <typename T>
+template <typename T, int MK>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const T* __restrict__ dout, const T* __restrict__ out,
+                                                                const float* __restrict__ rs,
+                                                                const float* __restrict__ rb,
                                                                 const T* __restrict__ y, const float* __restrict__ mean,
                                                                 const float* __restrict__ inv,
                                                                 const float* __restrict__ coef, T* __restrict__ dy,
@@ -398,15 +417,12 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const T* __restr
     const int c0 = (int)(i % cpr) * E;
     const int64_t off = i * E;
     float d[E], yy[E], r[E];
+    uint4 ov{};
     load_vec(dout + off, d);
-    if (out) {
-      float o[E];
-      load_vec(out + off, o);
-#pragma unroll
-      for (int e = 0; e < E; ++e) d[e] = o[e] > 0.f ? d[e] : 0.f;
-    }
-    if (dz_out) store_vec(dz_out + off, d);
+    if constexpr (MK == 1) ov = *reinterpret_cast<const uint4*>(out + off);
     load_vec(y + off, yy);
+    relu_mask<MK, T>(d, ov, yy, rs, rb, c0);
+    if (dz_out) store_vec(dz_out + off, d);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int c = c0 + e;
@@ -500,10 +516,13 @@ extern "C" int pose6d_bn_act_fwd(int32_t dtype, const void* y, const float* scal
 
 extern "C" int pose6d_bn_bwd_workspace_rows(int64_t M) { return p6::ceil_div(M, rows_per_block(M)); }
 
-extern "C" int pose6d_bn_bwd(int32_t dtype, const void* dout, const void* out, const void* y, const float* mean,
-                             const float* invstd, const float* gamma, float* dgamma, float* dbeta, int32_t accumulate,
-                             void* dy, void* dz_out, float* workspace, int64_t M, int32_t C, void* stream) {
+extern "C" int pose6d_bn_bwd(int32_t dtype, const void* dout, const void* out, const float* relu_scale,
+                             const float* relu_shift, const void* y, const float* mean, const float* invstd,
+                             const float* gamma, float* dgamma, float* dbeta, int32_t accumulate, void* dy,
+                             void* dz_out, float* workspace, int64_t M, int32_t C, void* stream) {
   P6_CHECK_ARG(C % 8 == 0 && M > 0, "pose6d_bn_bwd: bad sizes");
+  P6_CHECK_ARG(!relu_scale == !relu_shift, "pose6d_bn_bwd: relu_scale and relu_shift go together");
+  const int mk = out ? 1 : relu_scale ? 2 : 0;
   hipStream_t s = p6::stream_of(stream);
   const int rpb = rows_per_block(M);
   const int nb = p6::ceil_div(M, rpb);
@@ -514,25 +533,27 @@ extern "C" int pose6d_bn_bwd(int32_t dtype, const void* dout, const void* out, c
   const int cl = cpr < 64 ? cpr : 64;
   P6_CHECK_ARG(cpr % cl == 0 && kThreads % cl == 0, "pose6d_bn_bwd: C / vector width must be a power of two");
   dim3 grid(cpr / cl, nb);
-  if (dtype == POSE6D_DT_BF16) {
-    auto k = out ? bn_bwd_reduce2_kernel<bf16, true> : bn_bwd_reduce2_kernel<bf16, false>;
-    k<<<grid, kThreads, 0, s>>>((const bf16*)dout, (const bf16*)out, (const bf16*)y, mean, invstd, part, M, C, rpb);
-  } else {
-    auto k = out ? bn_bwd_reduce2_kernel<float, true> : bn_bwd_reduce2_kernel<float, false>;
-    k<<<grid, kThreads, 0, s>>>((const float*)dout, (const float*)out, (const float*)y, mean, invstd, part, M, C, rpb);
-  }
+  auto reduce = [&](auto* typed) {
+    using TT = std::remove_pointer_t<decltype(typed)>;
+    auto k = mk == 1 ? bn_bwd_reduce2_kernel<TT, 1> : mk == 2 ? bn_bwd_reduce2_kernel<TT, 2>
+                                                              : bn_bwd_reduce2_kernel<TT, 0>;
+    k<<<grid, kThreads, 0, s>>>((const TT*)dout, (const TT*)out, relu_scale, relu_shift, (const TT*)y, mean, invstd,
+                                part, M, C, rpb);
+  };
+  if (dtype == POSE6D_DT_BF16) reduce((bf16*)nullptr);
+  else reduce((float*)nullptr);
   P6_LAUNCH_CHECK();
   bn_bwd_finalize_kernel<<<p6::ceil_div(C, 16), kThreads, 0, s>>>(part, nb, C, (double)M, gamma, invstd, dgamma, dbeta,
                                                                   accumulate, coef);
   P6_LAUNCH_CHECK();
-  if (dtype == POSE6D_DT_BF16)
-    bn_bwd_apply_kernel<bf16><<<grid_for(M * C / 8), kThreads, 0, s>>>((const bf16*)dout, (const bf16*)out,
-                                                                         (const bf16*)y, mean, invstd, coef, (bf16*)dy,
-                                                                         (bf16*)dz_out, M, C);
-  else
-    bn_bwd_apply_kernel<float><<<grid_for(M * C / 4), kThreads, 0, s>>>((const float*)dout, (const float*)out,
-                                                                          (const float*)y, mean, invstd, coef,
-                                                                          (float*)dy, (float*)dz_out, M, C);
+  auto apply = [&](auto* typed) {
+    using TT = std::remove_pointer_t<decltype(typed)>;
+    auto k = mk == 1 ? bn_bwd_apply_kernel<TT, 1> : mk == 2 ? bn_bwd_apply_kernel<TT, 2> : bn_bwd_apply_kernel<TT, 0>;
+    k<<<grid_for(M * C / V<TT>::E), kThreads, 0, s>>>((const TT*)dout, (const TT*)out, relu_scale, relu_shift,
+                                                      (const TT*)y, mean, invstd, coef, (TT*)dy, (TT*)dz_out, M, C);
+  };
+  if (dtype == POSE6D_DT_BF16) apply((bf16*)nullptr);
+  else apply((float*)nullptr);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }

@@ -298,13 +298,17 @@ class TrunkEngine:
                 c = op.cop
                 M = B * c.Ho * c.Wo
                 bn = c.bn
-                call("bn_bwd", dt, op.out.g, op.out.t if op.relu else None, c.out.t, c.mean, c.inv,
-                     bn.weight.detach(), grad_of(bn.weight), grad_of(bn.bias), acc, c.out.g, op.dz, self.ws_bn, M,
-                     c.cout, st)
+                # ReLU mask: recomputed from the raw conv output when there is no residual
+                # (saves reading the forward output), read from it otherwise
+                plain = op.relu and op.res_act is None and op.res_conv is None
+                out = op.out.t if (op.relu and not plain) else None
+                rs, rb = (c.scale, c.shift) if plain else (None, None)
+                call("bn_bwd", dt, op.out.g, out, rs, rb, c.out.t, c.mean, c.inv, bn.weight.detach(),
+                     grad_of(bn.weight), grad_of(bn.bias), acc, c.out.g, op.dz, self.ws_bn, M, c.cout, st)
                 if op.res_conv is not None:
                     r = op.res_conv
                     # identity branch = bn_r(y_r) (no ReLU of its own): its dz is the masked dout
-                    call("bn_bwd", dt, op.dz, None, r.out.t, r.mean, r.inv, r.bn.weight.detach(),
+                    call("bn_bwd", dt, op.dz, None, None, None, r.out.t, r.mean, r.inv, r.bn.weight.detach(),
                          grad_of(r.bn.weight), grad_of(r.bn.bias), acc, r.out.g, None, self.ws_bn, M, r.cout, st)
                 elif op.res_act is not None:
                     op.res_act.pending = op.dz

@@ -183,13 +183,17 @@ int pose6d_bn_finalize(const float *partial, int32_t rows, int32_t C, int64_t co
 int pose6d_bn_act_fwd(int32_t dtype, const void *y, const float *scale, const float *shift, const void *res,
                       const float *res_scale, const float *res_shift, int32_t relu, void *out, int64_t M, int32_t C,
                       void *stream);
-/* backward of bn_act_fwd for one BN: dz = relu ? dout * (out > 0) : dout;
- * dgamma/dbeta (accumulate or overwrite); dy; dz_out (if non-NULL) = dz.
+/* backward of bn_act_fwd for one BN: dz = dout * mask, mask = out > 0 when `out` is
+ * given, else (relu_scale/relu_shift given: a ReLU BN without residual) the sign
+ * bn_act_fwd stored, recomputed from y as round(y * relu_scale + relu_shift) > 0
+ * (no read of the forward output), else 1; dgamma/dbeta (accumulate or
+ * overwrite); dy; dz_out (if non-NULL) = dz.
  * workspace: (pose6d_bn_bwd_workspace_rows(M) * 2 + 3) * C floats. */
 int pose6d_bn_bwd_workspace_rows(int64_t M);
-int pose6d_bn_bwd(int32_t dtype, const void *dout, const void *out, const void *y, const float *mean,
-                  const float *invstd, const float *gamma, float *dgamma, float *dbeta, int32_t accumulate, void *dy,
-                  void *dz_out, float *workspace, int64_t M, int32_t C, void *stream);
+int pose6d_bn_bwd(int32_t dtype, const void *dout, const void *out, const float *relu_scale,
+                  const float *relu_shift, const void *y, const float *mean, const float *invstd, const float *gamma,
+                  float *dgamma, float *dbeta, int32_t accumulate, void *dy, void *dz_out, float *workspace,
+                  int64_t M, int32_t C, void *stream);
 
 /* conv bias gradient: out[c] (+)= sum_m x[m][c] over an NHWC tensor of M pixels */
 int pose6d_channel_sum(int32_t dtype, const void *x, int64_t M, int32_t C, float *out, int32_t accumulate,

@@ -243,12 +243,25 @@ def test_bn_act_and_backward(dtype, C, N, H):
     dz = torch.empty_like(yd)
     dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
     for rep in range(2):
-        call("bn_bwd", dt, _nhwc(dout).to(dev, dtype), out, yd, mu, iv, gamma.to(dev), dg, db, 0, dy, dz, ws, M, C,
-             stream())
+        call("bn_bwd", dt, _nhwc(dout).to(dev, dtype), out, None, None, yd, mu, iv, gamma.to(dev), dg, db, 0, dy, dz,
+             ws, M, C, stream())
         if rep == 0:
             first = [t.clone() for t in (dy, dg, db)]
     for a, b in zip(first, (dy, dg, db)):
         assert torch.equal(a, b), "bn_bwd not repeatable"
+    # the same BN without residual: the ReLU mask recomputed from y (no forward output
+    # read) must equal the one read from the forward output, bit for bit
+    out2 = torch.empty_like(yd)
+    call("bn_act_fwd", dt, yd, sc, sh, None, None, None, 1, out2, M, C, stream())
+    got = []
+    for args in ((out2, None, None), (None, sc, sh)):
+        dy2, dz2 = torch.empty_like(yd), torch.empty_like(yd)
+        dg2, db2 = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        call("bn_bwd", dt, _nhwc(dout).to(dev, dtype), *args, yd, mu, iv, gamma.to(dev), dg2, db2, 0, dy2, dz2, ws, M,
+             C, stream())
+        got.append((dy2.cpu(), dz2.cpu(), dg2.cpu(), db2.cpu()))
+    for a, b in zip(*got):
+        assert torch.equal(a, b), "recomputed ReLU mask differs from the stored one"
     _close(dy.permute(0, 3, 1, 2), yr.grad, 1e-4 if dtype == torch.float32 else 3e-2, "bn dy")
     _close(dg, gr.grad, 1e-4 if dtype == torch.float32 else 3e-2, "dgamma")
     _close(db, br.grad, 1e-4 if dtype == torch.float32 else 3e-2, "dbeta")
