@@ -5,7 +5,7 @@ TAG=${1:-r}; shift
 OUT=$GRAFT_REPO_ROOT/gpurun_out
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
-timeout -k 10 900 python -m pytest tests -m gpu -q --timeout 400 -rf "$@" > $OUT/tests_$TAG.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -rf "$@" > $OUT/tests_$TAG.log 2>&1
 rc=$?; echo "tests rc=$rc" >> $OUT/tests_$TAG.log
 if [ $rc -gt 1 ] && [ $rc -ne 5 ]; then exit $rc; fi
 timeout -k 10 600 python bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || exit $?
