@@ -884,12 +884,29 @@ int launch_bwd_mode(int ds, const Geom& gd, const p6::WGeom& gw, const void* dy,
 // of 3) they run as ONE launch of conv_bwd_kernel, followed by the slab reduce;
 // otherwise as the separate pose6d_conv2d_dgrad + pose6d_conv2d_wgrad launches.
 // dx == NULL: weight gradient only.
+namespace {
+bool bwd_fused(const Plan& pd, const p6::WgradPlan& pw) {
+  return pd.fast && pd.tile == 3 && (pd.stages == 2 || pd.stages == 4) && pw.fast && pw.stages == 3 &&
+         getenv("POSE6D_BWD_SEPARATE") == nullptr;
+}
+}  // namespace
+
 extern "C" int pose6d_conv2d_backward(int32_t dtype, const void* x, const void* dy, const void* wt, const void* dres,
                                       void* dx, float* dw, int32_t accumulate, float* workspace, int64_t ws_bytes,
                                       int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout,
                                       int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
                                       void* stream) {
+  return pose6d_conv2d_backward_ex(dtype, x, dy, wt, dres, dx, dw, accumulate, workspace, ws_bytes, N, H, W, Cin,
+                                   Cin_real, Cout, KH, KW, stride, pad, Ho, Wo, 3, stream);
+}
+
+extern "C" int pose6d_conv2d_backward_ex(int32_t dtype, const void* x, const void* dy, const void* wt,
+                                         const void* dres, void* dx, float* dw, int32_t accumulate, float* workspace,
+                                         int64_t ws_bytes, int32_t N, int32_t H, int32_t W, int32_t Cin,
+                                         int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
+                                         int32_t pad, int32_t Ho, int32_t Wo, int32_t phases, void* stream) {
   P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_backward: bad dtype %d", dtype);
+  P6_CHECK_ARG(phases >= 1 && phases <= 3, "pose6d_conv2d_backward_ex: phases must be 1, 2 or 3");
   if (dx == nullptr)
     return pose6d_conv2d_wgrad(dtype, x, dy, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real, Cout, KH,
                                KW, stride, pad, Ho, Wo, stream);
@@ -901,9 +918,9 @@ extern "C" int pose6d_conv2d_backward(int32_t dtype, const void* x, const void* 
   const Plan pd = choose(dtype, mode, gd0);
   p6::WgradPlan pw;
   const p6::WGeom gw = p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
-  const bool fused = pd.fast && pd.tile == 3 && (pd.stages == 2 || pd.stages == 4) && pw.fast && pw.stages == 3 &&
-                     getenv("POSE6D_BWD_SEPARATE") == nullptr;
+  const bool fused = bwd_fused(pd, pw);
   if (!fused) {
+    if (!(phases & 1)) return POSE6D_OK;
     const int rc = pose6d_conv2d_dgrad(dtype, dy, wt, dres, dx, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo,
                                        stream);
     if (rc) return rc;
@@ -914,13 +931,15 @@ extern "C" int pose6d_conv2d_backward(int32_t dtype, const void* x, const void* 
                "pose6d_conv2d_backward: workspace %lld bytes < %lld needed", (long long)ws_bytes,
                (long long)pw.splits * Cout * gw.Kpad * 4);
   hipStream_t s = p6::stream_of(stream);
-  int rc;
-  switch (pd.mode) {
-    case kGemm: rc = launch_bwd_mode<kGemm>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, s); break;
-    case kDgradS2: rc = launch_bwd_mode<kDgradS2>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, s); break;
-    default: rc = launch_bwd_mode<kDgrad>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, s); break;
+  int rc = POSE6D_OK;
+  if (phases & 1) {
+    switch (pd.mode) {
+      case kGemm: rc = launch_bwd_mode<kGemm>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, s); break;
+      case kDgradS2: rc = launch_bwd_mode<kDgradS2>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, s); break;
+      default: rc = launch_bwd_mode<kDgrad>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, s); break;
+    }
   }
-  if (rc) return rc;
+  if (rc || !(phases & 2)) return rc;
   return p6::wgrad_reduce_launch(workspace, dw, Cout, gw.Kpad, Cin, Cin_real, KH, KW, gw.splits, accumulate, s);
 }
 
@@ -935,4 +954,17 @@ extern "C" int pose6d_conv_variant(int32_t dtype, int32_t pass, int32_t N, int32
                            : dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
   const Plan p = choose(dtype, mode, g);
   return (p.stages << 12) | ((int)p.fast << 8) | (p.mode << 4) | p.tile;
+}
+
+// fused backward variant (profiling joins): (1 << 16) | (dgrad mode << 4) | data-gradient
+// ring stages when pose6d_conv2d_backward runs ONE conv_bwd_kernel launch, else 0
+extern "C" int pose6d_bwd_variant(int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout,
+                                  int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo) {
+  if (Cin % 8 != 0 || ilog2(Cin) < 3) return 0;
+  int mode;
+  const Geom gd0 = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
+  const Plan pd = choose(dtype, mode, gd0);
+  p6::WgradPlan pw;
+  p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
+  return bwd_fused(pd, pw) ? (1 << 16) | (pd.mode << 4) | pd.stages : 0;
 }

@@ -22,8 +22,11 @@ def _sym(v, T):
     return f"conv_igemm_kernel<{T}, {bm}, {bn}, {mode}>"
 
 
-def conv_launches(eng):
-    """(symbol, flops, launch-callable) for every conv pass of one training step."""
+def conv_launches(eng, fused=True):
+    """(symbol, flops, launch-callable, name) for every conv pass of one training
+    step, issued the way the step issues them (fused=True: one conv_bwd_kernel
+    launch for the data + weight gradient where pose6d_conv2d_backward fuses them;
+    False: the separate dgrad and wgrad(+reduce) passes)."""
     B, dt, T = eng.B, eng.dt, _tname(eng.dtype)
     st = stream()
     out = []
@@ -38,6 +41,20 @@ def conv_launches(eng):
             call("conv2d_fwd", dt, op.src.t, op.wp, op.conv.bias, op.out.t, op.stats, B, op.H, op.W, op.cin_pad,
                  op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, st)
         out.append((sym, flops, fwd, op.name + ".fwd"))
+        bv = query("bwd_variant", dt, B, op.H, op.W, op.cin_pad, op.cout, op.k, op.k, op.stride, op.pad, op.Ho,
+                   op.Wo) if (op.needs_dgrad and fused) else 0
+        if bv:
+            # the step's fused data + weight gradient launch (conv2d_backward phase 1;
+            # the slab reduce is its own kernel and row in rocprof)
+            sym = f"conv_bwd_kernel<{(bv >> 4) & 15}, {bv & 15}, 3>"
+            dw = torch.empty_like(op.conv.weight)
+
+            def bwd(op=op, dw=dw):
+                call("conv2d_backward_ex", dt, op.src.t, op.out.g, op.wt, None, op.src.g, dw, 0, eng.ws_wgrad,
+                     eng.ws_wgrad.numel() * 4, B, op.H, op.W, op.cin_pad, op.cin, op.cout, op.k, op.k, op.stride,
+                     op.pad, op.Ho, op.Wo, 1, st)
+            out.append((sym, 2 * flops, bwd, op.name + ".bwd"))
+            continue
         if op.needs_dgrad:
             sym = _sym(query("conv_variant", dt, 1, B, op.H, op.W, op.cin_pad, op.cout, op.k, op.k, op.stride,
                              op.pad, op.Ho, op.Wo), T)

@@ -14,6 +14,7 @@ Prints ONE JSON line on rank 0 (contract in the task statement), including
 rank 0 only, bounded sample).
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -29,6 +30,9 @@ import torch  # noqa: E402
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0       # HBM3E spec
 FWD_BYTES_PER_CROP = 58.45e6   # bf16 fused-ideal forward bytes / crop
+FWD_BYTES_PER_CROP_F32 = 116.89e6   # the same forward in fp32
+PEAK_F32_VALU_TFLOPS = 157.3   # MI355X fp32 vector peak
+ADD_FLOPS_PER_PAIR = 8.0       # 3 sub, 1 mul, 2 fma per ADD-S pair
 
 
 def synth_batch(B, dev, seed):
@@ -90,6 +94,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-profile", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
+    ap.add_argument("--no-side", action="store_true", help="skip the configs[1] / configs[3] side measurements")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -147,6 +152,8 @@ def main():
     }
     if rank == 0 and not args.no_kernel_profile:
         result.update(kernel_profile(tr, ms))
+    if rank == 0 and not args.no_side:
+        result["side_configs"] = {"configs[1]": rgb_fp32_forward(dev), "configs[3]": add_eval_throughput(dev)}
     if rank == 0 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline()
@@ -171,9 +178,16 @@ def kernel_profile(tr, step_ms):
     # forward-only (training-mode BN) time of the trunk, graph-captured
     fwd_ms = forward_time(tr)
     fwd_gbs = FWD_BYTES_PER_CROP * tr.B / (fwd_ms * 1e-3) / 1e9
+    pmc, tsrc = pmc_traffic(sym)
+    traffic = round(pmc["hbm_bytes_per_launch"]) if pmc else None
+    # SQ_VALU_MFMA_BUSY_CYCLES = 16 cycles per 16x16x32 MFMA summed over the chip's
+    # 1024 SIMDs; busy fraction at the 2.4 GHz clock
+    mfma_busy = (round(pmc["mfma_busy_cycles_per_launch"] / (avg_t * 2.4e9 * 1024), 4)
+                 if pmc and "mfma_busy_cycles_per_launch" in pmc else None)
     return {
         "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+                     "traffic_source": tsrc, "mfma_busy": mfma_busy,
                      "kernel": sym, "launches_per_step": a["launches"],
                      "avg_launch_us": round(avg_t * 1e6, 2),
                      "algorithmic_flops_per_launch": a["flops"] / a["launches"]},
@@ -183,6 +197,76 @@ def kernel_profile(tr, step_ms):
                              "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(fwd_gbs / PEAK_HBM_GBS, 4),
                              "algorithmic_bytes_per_crop": FWD_BYTES_PER_CROP},
     }
+
+
+def pmc_traffic(sym):
+    """HBM bytes per launch of `sym` from the newest committed PMC summary
+    (profiles/*pmc*.json, made by tools/pmc_round.sh + tools/pmc_summary.py:
+    separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled for gfx950)."""
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            k = json.load(open(f))["kernels"].get(sym)
+        except (OSError, ValueError, KeyError):
+            continue
+        if k and "hbm_bytes_per_launch" in k:
+            return k, os.path.relpath(f, REPO)
+    return None, None
+
+
+def _time_fn(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e-3
+
+
+def rgb_fp32_forward(dev, B=32, reps=10):
+    """BASELINE configs[1]: PoseNetRGB bs32 224^2, fp32 (reference numerics), forward
+    of the drop-in module (eval mode, no autograd) -> crops/s and the HBM fraction
+    of SURVEY.md §8d's fp32 fused-ideal forward bytes."""
+    from models.pose_net_rgb import PoseNetRGB
+    torch.manual_seed(0)
+    m = PoseNetRGB(pretrained=False).to(dev).set_compute_dtype(torch.float32).eval()
+    x = torch.randn(B, 3, 224, 224, device=dev)
+    with torch.no_grad():
+        t = _time_fn(lambda: m(x), reps)
+    gbs = FWD_BYTES_PER_CROP_F32 * B / t / 1e9
+    return {"workload": "PoseNetRGB forward, eval mode, bs32 224^2, fp32", "value": round(B / t, 1),
+            "unit": "crops/s", "ms_per_batch": round(t * 1e3, 4), "dtype": "f32",
+            "hbm_roofline": {"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_bytes_per_crop": FWD_BYTES_PER_CROP_F32}}
+
+
+def add_eval_throughput(dev, B=256, N=2000, reps=10):
+    """BASELINE configs[3]: ADD/ADD-S eval of bs256 x 2000 mesh points x 13 objects
+    (SURVEY.md §8d synthetic meshes / perturbed poses) through ADDLoss.per_sample
+    (one pose6d_add_eval call) -> samples/s, ADD-S pairs/s, fraction of the fp32
+    vector peak at 8 flops per pair."""
+    import numpy as np
+    from models.add_loss import ADDLoss
+    from tests.synth import LINEMOD_OBJ_IDS, make_poses, synthetic_meshes
+    pts, diam = synthetic_meshes(N, seed=0)
+    crit = ADDLoss.__new__(ADDLoss)
+    torch.nn.Module.__init__(crit)
+    crit.points = {k: torch.from_numpy(v).to(dev) for k, v in pts.items()}
+    crit.diameters, crit.device, crit._table = diam, dev, None
+    rng = np.random.default_rng(0)
+    ids = np.array([LINEMOD_OBJ_IDS[i % len(LINEMOD_OBJ_IDS)] for i in range(B)], np.int64)
+    args = [torch.from_numpy(a).to(dev) for a in (*make_poses(rng, B), ids)]
+    t = _time_fn(lambda: crit.per_sample(*args), reps)
+    pairs = float(sum(pts[int(i)].shape[0] ** 2 for i in ids))
+    m = crit.eval_metrics(*args)
+    return {"workload": f"ADDLoss eval bs{B} x {N} pts x {len(pts)} objects (ADD, ADD-S, 0.1d)",
+            "value": round(B / t, 1), "unit": "samples/s", "ms_per_batch": round(t * 1e3, 4), "dtype": "f32",
+            "pairs_per_s": round(pairs / t, 1), "add_01d_acc": round(float(m["add_01d_acc"]), 3),
+            "valu_roofline": {"achieved": round(pairs * ADD_FLOPS_PER_PAIR / t / 1e12, 2), "peak": PEAK_F32_VALU_TFLOPS,
+                              "unit": "TFLOP/s",
+                              "frac": round(pairs * ADD_FLOPS_PER_PAIR / t / 1e12 / PEAK_F32_VALU_TFLOPS, 4)}}
 
 
 def forward_time(tr, reps=20):

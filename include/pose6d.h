@@ -167,6 +167,18 @@ int pose6d_conv2d_backward(int32_t dtype, const void *x, const void *dy, const v
                            void *dx, float *dw, int32_t accumulate, float *workspace, int64_t ws_bytes, int32_t N,
                            int32_t H, int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH,
                            int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, void *stream);
+/* pose6d_conv2d_backward in phases (profiling): bit 0 = the gradient launch(es) that
+ * fill the fp32 slabs (and dx), bit 1 = the slab reduce into dw; 3 = the whole call.
+ * On the unfused path bit 0 runs the complete dgrad + wgrad and bit 1 nothing. */
+int pose6d_conv2d_backward_ex(int32_t dtype, const void *x, const void *dy, const void *wt, const void *dres,
+                              void *dx, float *dw, int32_t accumulate, float *workspace, int64_t ws_bytes, int32_t N,
+                              int32_t H, int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH,
+                              int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, int32_t phases,
+                              void *stream);
+/* (1 << 16) | (data-gradient mode << 4) | ring stages when pose6d_conv2d_backward
+ * runs ONE fused conv_bwd_kernel<mode, stages, 3> launch (+ the reduce), else 0 */
+int pose6d_bwd_variant(int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH,
+                       int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo);
 
 /* nn.BatchNorm2d: finalize the conv-epilogue statistics (training) or use the
  * running statistics (eval) -> scale/shift (+ saved mean / invstd); running

@@ -32,6 +32,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--model", default="rgbd_geometric")
+    ap.add_argument("--eager", action="store_true", help="no hipGraph (PMC counter passes)")
     a = ap.parse_args()
     from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
     from pose6d.train import RGBDGeometricTrainer
@@ -40,7 +41,8 @@ def main():
     model = PoseNetRGBDGeometric(pretrained=False).to(dev)
     tr = RGBDGeometricTrainer(model, 32, dtype=torch.bfloat16)
     data = synth_batch(32, dev, seed=1000)
-    tr.capture(data)
+    if not a.eager:
+        tr.capture(data)
     for _ in range(3):
         tr.step(data)
     torch.cuda.synchronize()
