@@ -1,0 +1,90 @@
+"""Device-side input crops for the pose models: the per-sample body of the
+reference's LineMODDatasetRGBD / LineMODDatasetRGB.__getitem__
+(data/dataset_rgbd.py:85-206, data/dataset_rgb.py:83-147) after the file reads,
+batched into one pose6d_crop_rgbd launch.
+
+The host keeps what is cheap and must stay bit-identical: the bbox jitter is
+drawn with the reference's np.random calls in the reference's order
+(`jitter_bboxes`), the rotation-matrix -> quaternion conversion and labels stay
+with the caller.  Decoding the PNGs (cv2.imread) is I/O and stays on the host;
+the full frames are uploaded once per batch and everything after the read --
+padding, crop, resize, ToTensor/Normalize, depth normalisation, crop-adjusted
+centre and intrinsics -- runs on the GPU.
+
+Train-mode photometric augmentation of the reference's transform (ColorJitter,
+RandomErasing on PIL images, train_*.py:41-47) is not part of this path.
+"""
+import numpy as np
+import torch
+
+from ._lib import Pose6dError, call, require_device, stream
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def jitter_bboxes(bboxes, rgbd=True, rng=np.random):
+    """dataset_rgbd.py:110-118 (rgbd=True: +-5 % shift, +-10 % size) or
+    dataset_rgb.py:101-110 (+-15 %, +-20 %): four rng.uniform draws per sample in
+    the reference's order, int() truncation.  bboxes: (B, 4) ints -> (B, 4) int32."""
+    a, b = (0.05, 0.1) if rgbd else (0.15, 0.2)
+    out = np.zeros((len(bboxes), 4), np.int32)
+    for i, (x, y, w, h) in enumerate(np.asarray(bboxes).astype(np.int64).tolist()):
+        jx = int(rng.uniform(-a, a) * w)
+        jy = int(rng.uniform(-a, a) * h)
+        sw = int(rng.uniform(-b, b) * w)
+        sh = int(rng.uniform(-b, b) * h)
+        out[i] = (x + jx, y + jy, w + sw, h + sh)
+    return out
+
+
+class CropRGBD:
+    """Batched crop of full frames into the model inputs of the RGB-D datasets.
+
+    __call__(rgb, depth, bbox_orig, bbox_aug=None, K) with device tensors
+      rgb (B, H, W, 3) uint8 (RGB, or BGR with bgr=True), depth (B, H, W) uint16 mm
+      or int16/int32 holding mm values < 65536 (converted), or None;
+      bbox_orig / bbox_aug (B, 4) int (x, y, w, h); K (B, 3, 3) float
+    returns (rgb (B,3,S,S), depth (B,1,S,S), depth_raw (B,S,S), bbox_center (B,2),
+    camera_matrix (B,3,3)) -- the tensors dataset_rgbd.py:206 returns, batched.
+    """
+
+    def __init__(self, img_size=224, normalize=True, bgr=False, mean=IMAGENET_MEAN, std=IMAGENET_STD):
+        self.img_size = img_size
+        self.normalize = normalize
+        self.bgr = bgr
+        self._ms = torch.tensor(list(mean) + list(std), dtype=torch.float32)
+        self._ms_dev = {}
+
+    def _mean_std(self, dev):
+        if not self.normalize:
+            return None
+        t = self._ms_dev.get(dev)
+        if t is None:
+            t = self._ms_dev[dev] = self._ms.to(dev)
+        return t
+
+    def __call__(self, rgb, depth, bbox_orig, bbox_aug, K, out=None):
+        require_device(rgb, depth, bbox_orig, bbox_aug, K)
+        if rgb.dtype != torch.uint8 or rgb.dim() != 4 or rgb.shape[-1] != 3:
+            raise Pose6dError(f"CropRGBD: rgb must be (B, H, W, 3) uint8, got {tuple(rgb.shape)} {rgb.dtype}")
+        B, H, W, _ = rgb.shape
+        dev = rgb.device
+        if depth is not None:
+            if tuple(depth.shape) != (B, H, W):
+                raise Pose6dError(f"CropRGBD: depth must be (B, H, W) = {(B, H, W)}, got {tuple(depth.shape)}")
+            if depth.dtype != torch.uint16:
+                depth = depth.to(torch.int32).clamp_(0, 65535).to(torch.uint16)
+            depth = depth.contiguous()
+        if bbox_aug is None:
+            bbox_aug = bbox_orig
+        bo = bbox_orig.to(torch.int32).contiguous()
+        ba = bbox_aug.to(torch.int32).contiguous()
+        Kc = K.to(torch.float32).reshape(B, 3, 3).contiguous()
+        S = self.img_size
+        if out is None:
+            out = (torch.empty(B, 3, S, S, device=dev), torch.empty(B, 1, S, S, device=dev),
+                   torch.empty(B, S, S, device=dev), torch.empty(B, 2, device=dev), torch.empty(B, 3, 3, device=dev))
+        call("crop_rgbd", rgb.contiguous(), int(self.bgr), depth, B, H, W, bo, ba, Kc, S, self._mean_std(dev), *out,
+             stream())
+        return out

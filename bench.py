@@ -153,7 +153,8 @@ def main():
     if rank == 0 and not args.no_kernel_profile:
         result.update(kernel_profile(tr, ms))
     if rank == 0 and not args.no_side:
-        result["side_configs"] = {"configs[1]": rgb_fp32_forward(dev), "configs[3]": add_eval_throughput(dev)}
+        result["side_configs"] = {"configs[1]": rgb_fp32_forward(dev), "configs[3]": add_eval_throughput(dev),
+                                  "frame_crops": crop_throughput(dev)}
     if rank == 0 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline()
@@ -267,6 +268,41 @@ def add_eval_throughput(dev, B=256, N=2000, reps=10):
             "valu_roofline": {"achieved": round(pairs * ADD_FLOPS_PER_PAIR / t / 1e12, 2), "peak": PEAK_F32_VALU_TFLOPS,
                               "unit": "TFLOP/s",
                               "frac": round(pairs * ADD_FLOPS_PER_PAIR / t / 1e12 / PEAK_F32_VALU_TFLOPS, 4)}}
+
+
+def crop_throughput(dev, B=32, reps=20):
+    """North-star input path: 32 synthetic 640x480 frames (u8 RGB,
+    u16 depth 300-1600 mm), bbox w, h ~ U[40, 200] inside the frame, jittered as in
+    training -> pose6d_crop_rgbd (crop, pad, resize to 224, normalise, depth maps,
+    crop-adjusted centre / K); timed separately from the model step.  HBM bytes:
+    the source pixels the sampler touches (min(crop, 448)^2 clipped to the frame,
+    3 + 2 B each) + 224^2 * 20 B written per crop."""
+    import numpy as np
+    from pose6d.data import CropRGBD, jitter_bboxes
+    H, W, S = 480, 640, 224
+    rng = np.random.default_rng(0)
+    rgb = torch.from_numpy(rng.integers(0, 256, (B, H, W, 3), dtype=np.uint8)).to(dev)
+    depth = torch.from_numpy(rng.integers(300, 1601, (B, H, W), dtype=np.uint16)).to(dev)
+    w, h = rng.integers(40, 201, B), rng.integers(40, 201, B)
+    bo = np.stack([rng.integers(0, W - w), rng.integers(0, H - h), w, h], 1).astype(np.int32)
+    ba = jitter_bboxes(bo, True, np.random.RandomState(0))
+    K = torch.tensor([[572.4114, 0, 325.2611], [0, 573.57043, 242.04899], [0, 0, 1]]).expand(B, 3, 3).contiguous()
+    args = (rgb, depth, torch.from_numpy(bo).to(dev), torch.from_numpy(ba).to(dev), K.to(dev))
+    crop = CropRGBD(S)
+    out = crop(*args)
+    t = _time_fn(lambda: crop(*args, out=out), reps)
+    nbytes = 0
+    for x, y, ww, hh in ba.tolist():
+        size = max(ww, hh) * 1.2
+        n = int(size)
+        x1, y1 = int(x + ww / 2 - size / 2), int(y + hh / 2 - size / 2)
+        vis = max(0, min(W, x1 + n) - max(0, x1)) * max(0, min(H, y1 + n) - max(0, y1))
+        nbytes += vis * min(1.0, (2 * S / n) ** 2) * 5 + S * S * 20
+    gbs = nbytes / t / 1e9
+    return {"workload": f"pose6d_crop_rgbd: {B} frames 640x480 -> 224^2 model inputs (val transform)",
+            "value": round(B / t, 1), "unit": "crops/s", "ms_per_batch": round(t * 1e3, 4), "dtype": "u8/u16->f32",
+            "hbm_roofline": {"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_bytes_per_batch": round(nbytes)}}
 
 
 def forward_time(tr, reps=20):

@@ -109,6 +109,25 @@ int pose6d_pose_loss_bwd(const float *pred_rot, const float *pred_trans, const f
                          void *stream);
 
 /* ------------------------------------------------------------------------
+ * Input crops -- replaces the per-sample body of LineMODDatasetRGBD.__getitem__
+ * after the file reads (data/dataset_rgbd.py:104-206; dataset_rgb.py:95-145 for
+ * the RGB models): square crop x1.2 around the (jittered) bbox with zero padding,
+ * cv2.resize(..., (S, S)) INTER_LINEAR, ToTensor + Normalize, depth / 1000 and
+ * the (d - 0.1) / 1.5 normalisation, crop-adjusted centre and intrinsics.
+ * rgb [B][H][W][3] uint8 (RGB; bgr != 0: cv2.imread's BGR order, the
+ * cvtColor of dataset_rgbd.py:90 folded in); depth [B][H][W] uint16 mm or NULL
+ * (= zeros, :94-95); bbox_orig / bbox_aug [B][4] int32 (x, y, w, h) before /
+ * after the jitter of :110-118 (drawn on the host, np.random order); K [B][3][3].
+ * mean_std: 6 device floats (mean[3], std[3]) or NULL (ToTensor only).
+ * Outputs (each may be NULL): rgb_out [B][3][S][S], depth_out [B][1][S][S],
+ * depth_raw_out [B][S][S], center_out [B][2], K_out [B][3][3], all fp32.
+ * ---------------------------------------------------------------------- */
+int pose6d_crop_rgbd(const uint8_t *rgb, int32_t bgr, const uint16_t *depth, int32_t B, int32_t H, int32_t W,
+                     const int32_t *bbox_orig, const int32_t *bbox_aug, const float *K, int32_t S,
+                     const float *mean_std, float *rgb_out, float *depth_out, float *depth_raw_out,
+                     float *center_out, float *K_out, void *stream);
+
+/* ------------------------------------------------------------------------
  * ResNet50 trunk — replaces torchvision.models.resnet50 children[:-1] as
  * wrapped by every model (pose_net_rgb.py:18-20, pose_net_rgb_geometric.py:18-20,
  * pose_net_rgbd.py:48-61, pose_net_rgbd_geometric.py:23-25) and the z-CNN of
