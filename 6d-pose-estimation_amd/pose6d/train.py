@@ -52,10 +52,13 @@ class FlatArena:
     def grad_of(self, p):
         return self._views[id(p)]
 
-    def end_offset(self, p):
+    def _index_of(self, p):
         if not hasattr(self, "_index"):
             self._index = {id(q): i for i, q in enumerate(self.params)}
-        i = self._index[id(p)]
+        return self._index[id(p)]
+
+    def end_offset(self, p):
+        i = self._index_of(p)
         return self.offsets[i] + self.params[i].numel()
 
 
@@ -213,3 +216,59 @@ class RGBDGeometricTrainer:
 
     def set_lr(self, lr):
         self.hp[0].fill_(lr)
+
+    # ------------------------------------------------------------- checkpoints
+    def _torch_adamw(self):
+        lr, b1, b2, eps, wd = (float(v) for v in self.hp[:5].tolist())
+        return torch.optim.AdamW(self.model.parameters(), lr=lr, betas=(b1, b2), eps=eps, weight_decay=wd)
+
+    def optimizer_state_dict(self):
+        """The AdamW state as torch.optim.AdamW(model.parameters()).state_dict()
+        lays it out -- the `optimizer_state_dict` entry the reference's training
+        script saves and resumes from (train_rgbd_geometric.py:65,82,154)."""
+        opt = self._torch_adamw()
+        step = float(self.hp[5].item())
+        if step > 0:
+            for p in self.model.parameters():
+                o, n = self.arena.offsets[self.arena._index_of(p)], p.numel()
+                opt.state[p] = {"step": torch.tensor(step), "exp_avg": self.m[o:o + n].view_as(p).clone(),
+                                "exp_avg_sq": self.v[o:o + n].view_as(p).clone()}
+        return opt.state_dict()
+
+    def load_optimizer_state_dict(self, sd):
+        """Inverse of optimizer_state_dict(): accepts a torch AdamW state_dict over
+        model.parameters() (e.g. a reference checkpoint's optimizer_state_dict)."""
+        opt = self._torch_adamw()
+        opt.load_state_dict(sd)
+        g = opt.param_groups[0]
+        self.hp[:5].copy_(torch.tensor([g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"]]))
+        step = 0.0
+        with torch.no_grad():
+            self.m.zero_()
+            self.v.zero_()
+            for p in self.model.parameters():
+                st = opt.state.get(p)
+                if not st:
+                    continue
+                o, n = self.arena.offsets[self.arena._index_of(p)], p.numel()
+                self.m[o:o + n].copy_(st["exp_avg"].reshape(-1))
+                self.v[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+                step = float(st["step"])
+        self.hp[5].fill_(step)
+
+    def checkpoint(self, epoch, best_acc=0.0, curr_acc=0.0, **extra):
+        """The reference's checkpoint dict (train_rgbd_geometric.py:151-157): model
+        state_dict with the reference's keys (OIHW fp32 masters), torch-AdamW
+        optimizer state, epoch, best / current accuracy (+ e.g. curr_add)."""
+        return {"epoch": epoch, "model_state_dict": self.model.state_dict(),
+                "optimizer_state_dict": self.optimizer_state_dict(), "best_acc": best_acc, "curr_acc": curr_acc,
+                **extra}
+
+    def load_checkpoint(self, ckpt):
+        """Resume from a reference-format checkpoint (train_rgbd_geometric.py:79-84):
+        parameters / BN buffers are copied into the flat arena in place, so the
+        captured graph keeps running on them.  Returns the next epoch."""
+        self.model.load_state_dict(ckpt["model_state_dict"])
+        if "optimizer_state_dict" in ckpt:
+            self.load_optimizer_state_dict(ckpt["optimizer_state_dict"])
+        return ckpt.get("epoch", -1) + 1
