@@ -4,6 +4,8 @@
 // pose_net_rgb.py:23-50, pose_net_rgb_geometric.py:23-33,58-65,
 // pose_net_rgbd_geometric.py:28-38.  M (batch) is 32 per GPU, so these are skinny
 // GEMMs bound by reading the weight matrix once (8 MB for 2048x1024 fp32).
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -72,6 +74,134 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(const float* __restr
     }
 }
 
+// Skinny Linear GEMMs (the batch M <= 32 is the small side) on MFMA f32 16x16x4:
+// C[M][N] = alpha * A B (+ bias) + beta * C with A(m, k) = A[m * sam + k] and
+// B(k, n) = B[n * sbn + k] (BKC: the nn.Linear weight [N][K], forward) or
+// B[k * sbk + n] (data gradient through the weight).  One workgroup per 16
+// output columns; its 16 waves split K and meet in LDS (fixed wave order, no
+// workspace, one launch): every weight byte is read once, by 4-byte-per-lane
+// rows of 64 B.  Inside a 16-deep K chunk lane (r, q) feeds MFMA step s with
+// k = 4 q + s, so A and (BKC) B fragments are single 16-byte loads; the
+// reduction order differs from torch's but all products are exact fp32.
+constexpr int kSkW = 16;                      // waves per workgroup
+constexpr int kSkThreads = kSkW * 64;
+
+template <bool BKC, bool VEC>
+__global__ __launch_bounds__(kSkThreads) void skinny_gemm_kernel(
+    const float* __restrict__ A, int64_t sam, const float* __restrict__ B, int64_t sbk, int64_t sbn,
+    float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, int M, int N, int K, float alpha, float beta) {
+  __shared__ float red[kSkW][32][17];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int n0 = blockIdx.x * 16, n = n0 + r;
+  const int kc = ((K + kSkW - 1) / kSkW + 15) & ~15;
+  const int kb = w * kc, ke = min(K, kb + kc);
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const bool m0ok = r < M, m1ok = r + 16 < M, nok = n < N;
+  for (int k = kb; k < ke; k += 16) {
+    const int kq = k + 4 * q;
+    float a0[4], a1[4], b[4];
+    if (VEC && kq + 3 < ke) {
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 va0 = m0ok ? *reinterpret_cast<const f32x4*>(A + r * sam + kq) : z;
+      const f32x4 va1 = m1ok ? *reinterpret_cast<const f32x4*>(A + (r + 16) * sam + kq) : z;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) { a0[s] = va0[s]; a1[s] = va1[s]; }
+      if (BKC) {
+        const f32x4 vb = nok ? *reinterpret_cast<const f32x4*>(B + n * sbn + kq) : z;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) b[s] = vb[s];
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) b[s] = nok ? B[(int64_t)(kq + s) * sbk + n] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int kk = kq + s;
+        const bool kok = kk < ke;
+        a0[s] = (kok && m0ok) ? A[r * sam + kk] : 0.f;
+        a1[s] = (kok && m1ok) ? A[(r + 16) * sam + kk] : 0.f;
+        b[s] = (kok && nok) ? (BKC ? B[n * sbn + kk] : B[(int64_t)kk * sbk + n]) : 0.f;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], b[s], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s], b[s], acc1, 0, 0, 0);
+    }
+  }
+  // lane holds rows 4q + i (+16) of column r
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    red[w][4 * q + i][r] = acc0[i];
+    red[w][16 + 4 * q + i][r] = acc1[i];
+  }
+  __syncthreads();
+  if (threadIdx.x < 32 * 16) {
+    const int mm = threadIdx.x >> 4, cc = threadIdx.x & 15, nn = n0 + cc;
+    if (mm < M && nn < N) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < kSkW; ++i) t += red[i][mm][cc];
+      float v = alpha * t;
+      if (bias) v += bias[nn];
+      if (beta != 0.f) v += beta * C[mm * ldc + nn];
+      C[mm * ldc + nn] = v;
+    }
+  }
+}
+
+// nn.Linear weight / bias gradient: dW[n][k] (+)= sum_b dy[b][n] x[b][k] and
+// db[n] (+)= sum_b dy[b][n] (the batch, <= a few hundred rows, is the contraction).
+// Block = 16 output rows n x 256 columns k; thread = 4 n x 4 k (one float4 of x and
+// four broadcast dy values per batch row); the blocks of column tile 0 also write db.
+__global__ __launch_bounds__(kThreads) void linear_wgrad_kernel(const float* __restrict__ dy, int64_t ldy,
+                                                                const float* __restrict__ x, int64_t ldx,
+                                                                float* __restrict__ dw, float* __restrict__ db, int N,
+                                                                int K, int Bn, int accumulate, int xvec, int wvec) {
+  const int kq = threadIdx.x & 63, ng = threadIdx.x >> 6;
+  const int k0 = blockIdx.x * 256 + 4 * kq;
+  const int nb = blockIdx.y * 16 + 4 * ng;
+  float acc[4][4] = {};
+  float bs[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool vec = xvec && k0 + 3 < K;
+  for (int b = 0; b < Bn; ++b) {
+    float xv[4];
+    if (vec) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(x + b * ldx + k0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xv[j] = v[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xv[j] = k0 + j < K ? x[b * ldx + k0 + j] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float d = nb + i < N ? dy[b * ldy + nb + i] : 0.f;
+      bs[i] += d;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(d, xv[j], acc[i][j]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int nn = nb + i;
+    if (nn >= N) continue;
+    float* o = dw + (int64_t)nn * K + k0;
+    if (wvec && k0 + 3 < K) {
+      f32x4 v = {acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
+      if (accumulate) v += *reinterpret_cast<const f32x4*>(o);
+      *reinterpret_cast<f32x4*>(o) = v;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (k0 + j < K) o[j] = accumulate ? o[j] + acc[i][j] : acc[i][j];
+    }
+    if (db && blockIdx.x == 0 && kq == 0) db[nn] = accumulate ? db[nn] + bs[i] : bs[i];
+  }
+}
+
 // C[m][n] = alpha * sum_z part[z][m][n] (+ bias[n]) + beta * C[m][n]   (fixed order)
 __global__ void gemm_splitk_reduce_kernel(const float* __restrict__ part, int splits, float* __restrict__ C,
                                           int64_t ldc, const float* __restrict__ bias, int M, int N, float alpha,
@@ -99,36 +229,60 @@ __global__ void colsum_kernel(const float* __restrict__ dy, int64_t ldy, float* 
 
 using p6::uniform01;
 
-// BatchNorm1d over the batch (one thread per column) + optional ReLU + Dropout.
-__global__ void bn1d_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int M, int C,
-                                const float* __restrict__ gamma, const float* __restrict__ beta,
-                                float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
-                                float momentum, float eps, int training, int relu, float p_drop, const uint64_t* __restrict__ seedp, uint64_t salt,
-                                uint8_t* __restrict__ mask, float* __restrict__ smean, float* __restrict__ sinv) {
-  const int c = blockIdx.x * kThreads + threadIdx.x;
-  if (c >= C) return;
+// BatchNorm1d over the batch + optional ReLU + Dropout.  Block = 64 columns (one
+// per lane: coalesced rows) x 4 row groups (one per wave, rows g, g+4, ...); the
+// per-group fp64 sums meet in LDS and are combined in group order (deterministic).
+constexpr int kBnCols = 64, kBnGroups = kThreads / kBnCols;
+
+__device__ __forceinline__ double group_total(double v, double (*red)[kBnCols], int g, int cl) {
+  red[g][cl] = v;
+  __syncthreads();
+  double t = 0.0;
+#pragma unroll
+  for (int i = 0; i < kBnGroups; ++i) t += red[i][cl];
+  __syncthreads();
+  return t;
+}
+
+__global__ __launch_bounds__(kThreads) void bn1d_fwd_kernel(
+    const float* __restrict__ x, float* __restrict__ y, int M, int C, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
+    float momentum, float eps, int training, int relu, float p_drop, const uint64_t* __restrict__ seedp, uint64_t salt,
+    uint8_t* __restrict__ mask, float* __restrict__ smean, float* __restrict__ sinv) {
+  __shared__ double red[kBnGroups][kBnCols];
+  const int cl = threadIdx.x % kBnCols, g = threadIdx.x / kBnCols;
+  const int c = blockIdx.x * kBnCols + cl;
+  const bool ok = c < C;
   float mean, inv;
   if (training) {
-    double s = 0.0, q = 0.0;
-    for (int m = 0; m < M; ++m) s += x[(int64_t)m * C + c];
-    mean = (float)(s / M);
-    for (int m = 0; m < M; ++m) { const double d = x[(int64_t)m * C + c] - mean; q += d * d; }
-    const double var = q / M;
+    double s = 0.0;
+    if (ok)
+      for (int m = g; m < M; m += kBnGroups) s += x[(int64_t)m * C + c];
+    mean = (float)(group_total(s, red, g, cl) / M);
+    double q = 0.0;
+    if (ok)
+      for (int m = g; m < M; m += kBnGroups) { const double d = x[(int64_t)m * C + c] - mean; q += d * d; }
+    const double var = group_total(q, red, g, cl) / M;
     inv = (float)(1.0 / sqrt(var + eps));
-    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
-    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(M > 1 ? var * M / (M - 1) : var);
-    if (c == 0 && nbt) nbt[0] += 1;
+    if (ok && g == 0) {
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(M > 1 ? var * M / (M - 1) : var);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) nbt[0] += 1;
   } else {
-    mean = rmean[c];
-    inv = 1.0f / sqrtf(rvar[c] + eps);
+    mean = ok ? rmean[c] : 0.f;
+    inv = ok ? 1.0f / sqrtf(rvar[c] + eps) : 0.f;
   }
-  smean[c] = mean;
-  sinv[c] = inv;
-  const float g = gamma[c], b = beta[c];
+  if (!ok) return;
+  if (g == 0) {
+    smean[c] = mean;
+    sinv[c] = inv;
+  }
+  const float gm = gamma[c], b = beta[c];
   const float keep_scale = p_drop > 0.f ? 1.0f / (1.0f - p_drop) : 1.0f;
-  for (int m = 0; m < M; ++m) {
+  for (int m = g; m < M; m += kBnGroups) {
     const int64_t o = (int64_t)m * C + c;
-    float v = (x[o] - mean) * inv * g + b;
+    float v = (x[o] - mean) * inv * gm + b;
     if (relu) v = fmaxf(v, 0.f);
     if (p_drop > 0.f) {
       const bool keep = uniform01(seedp[0] ^ salt, (uint64_t)o) >= p_drop;
@@ -139,35 +293,45 @@ __global__ void bn1d_fwd_kernel(const float* __restrict__ x, float* __restrict__
   }
 }
 
-// backward of bn1d_fwd (train mode: batch statistics)
-__global__ void bn1d_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
-                                const float* __restrict__ y, int M, int C, const float* __restrict__ gamma,
-                                const float* __restrict__ smean, const float* __restrict__ sinv, int training,
-                                int relu, float p_drop, const uint8_t* __restrict__ mask, float* __restrict__ dx,
-                                float* __restrict__ dgamma, float* __restrict__ dbeta, int accumulate) {
-  const int c = blockIdx.x * kThreads + threadIdx.x;
-  if (c >= C) return;
-  const float mean = smean[c], inv = sinv[c], g = gamma[c];
+// backward of bn1d_fwd (train mode: batch statistics), same block shape
+__global__ __launch_bounds__(kThreads) void bn1d_bwd_kernel(
+    const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ y, int M, int C,
+    const float* __restrict__ gamma, const float* __restrict__ smean, const float* __restrict__ sinv, int training,
+    int relu, float p_drop, const uint8_t* __restrict__ mask, float* __restrict__ dx, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, int accumulate) {
+  __shared__ double red[kBnGroups][kBnCols];
+  const int cl = threadIdx.x % kBnCols, g = threadIdx.x / kBnCols;
+  const int c = blockIdx.x * kBnCols + cl;
+  const bool ok = c < C;
+  const float mean = ok ? smean[c] : 0.f, inv = ok ? sinv[c] : 0.f, gm = ok ? gamma[c] : 0.f;
   const float keep_scale = p_drop > 0.f ? 1.0f / (1.0f - p_drop) : 1.0f;
+  auto grad_in = [&](int64_t o) {
+    float d = dy[o];
+    if (p_drop > 0.f) d = mask[o] ? d * keep_scale : 0.f;
+    if (relu && !(y[o] > 0.f)) d = 0.f;
+    return d;
+  };
   double sd = 0.0, sdx = 0.0;
-  for (int m = 0; m < M; ++m) {
-    const int64_t o = (int64_t)m * C + c;
-    float d = dy[o];
-    if (p_drop > 0.f) d = mask[o] ? d * keep_scale : 0.f;
-    if (relu && !(y[o] > 0.f)) d = 0.f;
-    sd += d;
-    sdx += (double)d * ((x[o] - mean) * inv);
+  if (ok)
+    for (int m = g; m < M; m += kBnGroups) {
+      const int64_t o = (int64_t)m * C + c;
+      const float d = grad_in(o);
+      sd += d;
+      sdx += (double)d * ((x[o] - mean) * inv);
+    }
+  sd = group_total(sd, red, g, cl);
+  sdx = group_total(sdx, red, g, cl);
+  if (!ok) return;
+  if (g == 0) {
+    if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)sdx;
+    if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)sd;
   }
-  if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)sdx;
-  if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)sd;
   const float c2 = (float)(sd / M), c3 = (float)(sdx / M);
-  for (int m = 0; m < M; ++m) {
+  for (int m = g; m < M; m += kBnGroups) {
     const int64_t o = (int64_t)m * C + c;
-    float d = dy[o];
-    if (p_drop > 0.f) d = mask[o] ? d * keep_scale : 0.f;
-    if (relu && !(y[o] > 0.f)) d = 0.f;
+    const float d = grad_in(o);
     const float xh = (x[o] - mean) * inv;
-    dx[o] = training ? g * inv * (d - c2 - xh * c3) : g * inv * d;
+    dx[o] = training ? gm * inv * (d - c2 - xh * c3) : gm * inv * d;
   }
 }
 
@@ -211,6 +375,26 @@ extern "C" int pose6d_gemm_f32(const float* A, int64_t sam, int64_t sak, const f
   P6_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "pose6d_gemm_f32: bad sizes");
   if (M == 0 || N == 0) return POSE6D_OK;
   hipStream_t s = p6::stream_of(stream);
+  // batch-side skinny GEMMs (nn.Linear forward / data gradient): MFMA kernel
+  const bool bkc = sbk == 1, bnc = sbn == 1;
+  if (M <= 32 && sak == 1 && (bkc || bnc) && getenv("POSE6D_HEAD_GENERIC") == nullptr) {
+    const bool vec = ((uintptr_t)A & 15) == 0 && (sam & 3) == 0 && (K & 3) == 0 &&
+                     (!bkc || (((uintptr_t)B & 15) == 0 && (sbn & 3) == 0));
+    const dim3 grid(p6::ceil_div(N, 16));
+    if (bkc) {
+      if (vec) skinny_gemm_kernel<true, true><<<grid, kSkThreads, 0, s>>>(A, sam, B, sbk, sbn, C, ldc, bias, M, N, K,
+                                                                          alpha, beta);
+      else skinny_gemm_kernel<true, false><<<grid, kSkThreads, 0, s>>>(A, sam, B, sbk, sbn, C, ldc, bias, M, N, K,
+                                                                        alpha, beta);
+    } else {
+      if (vec) skinny_gemm_kernel<false, true><<<grid, kSkThreads, 0, s>>>(A, sam, B, sbk, sbn, C, ldc, bias, M, N, K,
+                                                                           alpha, beta);
+      else skinny_gemm_kernel<false, false><<<grid, kSkThreads, 0, s>>>(A, sam, B, sbk, sbn, C, ldc, bias, M, N, K,
+                                                                         alpha, beta);
+    }
+    P6_LAUNCH_CHECK();
+    return POSE6D_OK;
+  }
   const int tiles = p6::ceil_div(N, TBN) * p6::ceil_div(M, TBM);
   // skinny (batch-32) GEMMs: split K so that >= ~256 workgroups stream the weights
   int splits = 1;
@@ -252,7 +436,7 @@ extern "C" int pose6d_bn1d_fwd(const float* x, float* y, int32_t M, int32_t C, c
   P6_CHECK_ARG(M > 0 && C > 0, "pose6d_bn1d_fwd: bad sizes");
   P6_CHECK_ARG(!training || M > 1, "Expected more than 1 value per channel when training (BatchNorm1d)");
   P6_CHECK_ARG(p_drop == 0.f || (mask && seed), "pose6d_bn1d_fwd: dropout needs a mask buffer and a seed");
-  bn1d_fwd_kernel<<<p6::ceil_div(C, kThreads), kThreads, 0, p6::stream_of(stream)>>>(
+  bn1d_fwd_kernel<<<p6::ceil_div(C, kBnCols), kThreads, 0, p6::stream_of(stream)>>>(
       x, y, M, C, gamma, beta, running_mean, running_var, num_batches, momentum, eps, training, relu, p_drop, seed, salt,
       mask, save_mean, save_invstd);
   P6_LAUNCH_CHECK();
@@ -263,7 +447,7 @@ extern "C" int pose6d_bn1d_bwd(const float* dy, const float* x, const float* y, 
                                const float* gamma, const float* save_mean, const float* save_invstd, int32_t training,
                                int32_t relu, float p_drop, const uint8_t* mask, float* dx, float* dgamma, float* dbeta,
                                int32_t accumulate, void* stream) {
-  bn1d_bwd_kernel<<<p6::ceil_div(C, kThreads), kThreads, 0, p6::stream_of(stream)>>>(
+  bn1d_bwd_kernel<<<p6::ceil_div(C, kBnCols), kThreads, 0, p6::stream_of(stream)>>>(
       dy, x, y, M, C, gamma, save_mean, save_invstd, training, relu, p_drop, mask, dx, dgamma, dbeta, accumulate);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
@@ -284,6 +468,18 @@ extern "C" int pose6d_act_bwd(const float* dy, const float* x, float* dx, int64_
   if (n == 0) return POSE6D_OK;
   act_bwd_kernel<<<(unsigned)((n + kThreads - 1) / kThreads), kThreads, 0, p6::stream_of(stream)>>>(dy, x, dx, n, act,
                                                                                                  p_drop, mask);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+extern "C" int pose6d_linear_wgrad(const float* dy, int64_t ldy, const float* x, int64_t ldx, float* dw, float* db,
+                                   int32_t N, int32_t K, int32_t B, int32_t accumulate, void* stream) {
+  P6_CHECK_ARG(N > 0 && K > 0 && B >= 0 && ldy >= N && ldx >= K, "pose6d_linear_wgrad: bad shape");
+  const dim3 grid(p6::ceil_div(K, 256), p6::ceil_div(N, 16));
+  const int xvec = ((uintptr_t)x & 15) == 0 && (ldx & 3) == 0;
+  const int wvec = ((uintptr_t)dw & 15) == 0 && (K & 3) == 0;
+  linear_wgrad_kernel<<<grid, kThreads, 0, p6::stream_of(stream)>>>(dy, ldy, x, ldx, dw, db, N, K, B, accumulate,
+                                                                    xvec, wvec);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }

@@ -98,9 +98,7 @@ class FusionEngine:
         """dW (+)= dy^T x, db (+)= colsum(dy), dx = dy W (+ dx_beta * dx)."""
         B = dy.shape[0]
         N, K = lin.out_features, lin.in_features
-        call("gemm_f32", dy, 1, lddy, x, ldx, 1, grad_of(lin.weight), K, None, N, K, B, 1.0, float(acc), self.ws,
-             self.ws.numel(), st)
-        call("colsum_f32", dy, lddy, grad_of(lin.bias), B, N, acc, st)
+        call("linear_wgrad", dy, lddy, x, ldx, grad_of(lin.weight), grad_of(lin.bias), N, K, B, acc, st)
         if dx is not None:
             call("gemm_f32", dy, lddy, 1, lin.weight.detach(), K, 1, dx, K, None, B, K, N, 1.0, dx_beta, self.ws,
                  self.ws.numel(), st)

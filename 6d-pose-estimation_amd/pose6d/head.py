@@ -164,11 +164,9 @@ class HeadEngine:
             if st.kind == "linear":
                 m = st.mod
                 K, N = m.in_features, m.out_features
-                # dW[N][K] = dy^T x
-                call("gemm_f32", g, 1, N, st.x, K, 1, grad_of(m.weight), K, None, N, K, B, 1.0, float(acc),
-                     self.ws, self.ws.numel(), st_)
-                if m.bias is not None:
-                    call("colsum_f32", g, N, grad_of(m.bias), B, N, acc, st_)
+                # dW[N][K] = dy^T x and db = colsum(dy), one launch
+                call("linear_wgrad", g, N, st.x, K, grad_of(m.weight),
+                     grad_of(m.bias) if m.bias is not None else None, N, K, B, acc, st_)
                 if last and not need_dx:
                     return None
                 call("gemm_f32", g, N, 1, m.weight.detach(), K, 1, st.dx, K, None, B, K, N, 1.0, 0.0, self.ws,

@@ -250,6 +250,10 @@ int pose6d_avgpool_bwd(int32_t dtype, const float *dy, void *dx, int32_t N, int3
 int pose6d_gemm_f32(const float *A, int64_t sam, int64_t sak, const float *B, int64_t sbk, int64_t sbn, float *C,
                     int64_t ldc, const float *bias, int32_t M, int32_t N, int32_t K, float alpha, float beta,
                     float *workspace, int64_t ws_floats, void *stream);
+/* nn.Linear parameter gradients in one launch: dW[n][k] (+)= sum_b dy[b*ldy + n] x[b*ldx + k],
+ * db[n] (+)= sum_b dy[b*ldy + n] (db may be NULL); dW [N][K] contiguous. */
+int pose6d_linear_wgrad(const float *dy, int64_t ldy, const float *x, int64_t ldx, float *dw, float *db, int32_t N,
+                        int32_t K, int32_t B, int32_t accumulate, void *stream);
 /* db[n] (+)= sum_m dy[m * ldy + n]  (Linear bias gradient; ldy >= N) */
 int pose6d_colsum_f32(const float *dy, int64_t ldy, float *db, int32_t M, int32_t N, int32_t accumulate,
                       void *stream);
