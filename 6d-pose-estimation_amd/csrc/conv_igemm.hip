@@ -43,6 +43,7 @@ struct Geom {
   int RH, RW;              // row grid: m = (n * RH + y) * RW + x
   int KH, KW, stride, pad;
   int gm, gn;              // grid in tiles
+  int nmajor;              // fast path: tile order N-major (weights larger than the gathered source)
 };
 
 // ds_read_b128 fragment reads: lanes (row = l & 15, chunk = l >> 4) of a 16-row
@@ -416,7 +417,11 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
     ntx = (g.KW - kw0 + 1) >> 1;
     nk = (nty * ntx) << (g.log2SC - 6);
   }
-  const int tm = bid / g.gn, tn = bid - tm * g.gn;
+  // consecutive logical tiles share an XCD (remap above): M-major keeps a few A row
+  // blocks + all of B in that XCD's L2, N-major all of A + a slice of B
+  int tm, tn;
+  if (g.nmajor) { tn = bid / g.gm; tm = bid - tn * g.gm; }
+  else { tm = bid / g.gn; tn = bid - tm * g.gn; }
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -767,6 +772,12 @@ Plan choose(int dtype, int mode, const Geom& g) {
     p.g.RH = g.RH / 2;
     p.g.RW = g.RW / 2;
   }
+  {
+    // POSE6D_CONV_ORDER=n: N-major tile order (A/B experiments; measured neutral on
+    // every ResNet50 layer at batch 32 -- footprints fit L2 either way)
+    const char* ord = getenv("POSE6D_CONV_ORDER");
+    p.g.nmajor = ord && ord[0] == 'n';
+  }
   p.tile = env_int("POSE6D_CONV_TILE", pick_tile_fast(p.g.M, g.Ncols, p.mode == kDgradS2 ? 4 : 1));
   if (p.tile == 2) p.tile = 3;   // no 64x128 instance on the fast path
   // two slots (32 KiB at 64x64) keep several workgroups per CU resident, which hides
@@ -908,7 +919,7 @@ extern "C" int pose6d_conv2d_backward_ex(int32_t dtype, const void* x, const voi
   P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_backward: bad dtype %d", dtype);
   P6_CHECK_ARG(phases >= 1 && phases <= 3, "pose6d_conv2d_backward_ex: phases must be 1, 2 or 3");
   if (dx == nullptr)
-    return pose6d_conv2d_wgrad(dtype, x, dy, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real, Cout, KH,
+    return !(phases & 1) ? POSE6D_OK : pose6d_conv2d_wgrad(dtype, x, dy, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real, Cout, KH,
                                KW, stride, pad, Ho, Wo, stream);
   P6_CHECK_ARG(stride == 1 || stride == 2, "pose6d_conv2d_backward: stride must be 1 or 2");
   P6_CHECK_ARG(Cin % 8 == 0 && Cin_real <= Cin && ilog2(Cin) >= 3,
