@@ -384,6 +384,32 @@ __device__ __forceinline__ void lds_read_frags(u32x4 (&f)[NR], const unsigned (&
   }
 }
 
+// Both k-halves of a 64x64 tile's fragments (2 x 4 ds_read_b128) issued as ONE asm
+// batch without a wait; lds_wait_first / lds_wait_all then release them in two
+// steps (counted lgkmcnt), so the second half's reads are in flight while the
+// first half's MFMAs run.  The waits name the fragments as in-out operands: the
+// compiler cannot hoist an MFMA that consumes them above the wait.
+__device__ __forceinline__ void lds_issue_frags8(u32x4 (&f)[2][4], const unsigned (&a)[2][4]) {
+  asm volatile(
+      "ds_read_b128 %0, %8\n\tds_read_b128 %1, %9\n\tds_read_b128 %2, %10\n\tds_read_b128 %3, %11\n\t"
+      "ds_read_b128 %4, %12\n\tds_read_b128 %5, %13\n\tds_read_b128 %6, %14\n\tds_read_b128 %7, %15"
+      : "=&v"(f[0][0]), "=&v"(f[0][1]), "=&v"(f[0][2]), "=&v"(f[0][3]), "=&v"(f[1][0]), "=&v"(f[1][1]),
+        "=&v"(f[1][2]), "=&v"(f[1][3])
+      : "v"(a[0][0]), "v"(a[0][1]), "v"(a[0][2]), "v"(a[0][3]), "v"(a[1][0]), "v"(a[1][1]), "v"(a[1][2]),
+        "v"(a[1][3]));
+}
+__device__ __forceinline__ void lds_wait_first(u32x4 (&f)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
+}
+__device__ __forceinline__ void lds_wait_all(u32x4 (&f)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
+}
+
+#ifndef POSE6D_PAIRED_FRAGS
+#define POSE6D_PAIRED_FRAGS 1
+#endif
+constexpr bool kPairedFrags = POSE6D_PAIRED_FRAGS;
+
 // one workgroup's work; `bid_in` = its index in this conv's sub-grid (the whole grid,
 // or the leading part of a fused backward launch), `smem` = the kernel's dynamic LDS
 template <int BM, int BN, int MODE, int S>
@@ -450,43 +476,37 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
       else { a_y[i] = y * g.stride - g.pad; a_x[i] = x * g.stride - g.pad; }
     }
   }
-  const bf16* b_src[B_INS];
+  // B rows: n >= Ncols read the zero page (offset masked to 0)
+  const bf16* b_base[B_INS];
+  unsigned b_mask[B_INS];
 #pragma unroll
   for (int j = 0; j < B_INS; ++j) {
     const int row = j * 32 + wave * 8 + r8;
     const int n = n0 + row;
-    b_src[j] = n < g.Ncols ? wts + (int64_t)n * g.Kpad + (pch ^ swz8(row)) * 8 : nullptr;
+    const bool ok = n < g.Ncols;
+    b_base[j] = ok ? wts + (int64_t)n * g.Kpad + (pch ^ swz8(row)) * 8 : reinterpret_cast<const bf16*>(zp);
+    b_mask[j] = ok ? ~0u : 0u;
   }
 
-  auto issue = [&](int kt, int buf) {
-    const int k0 = kt * 64;
-    char* As = smem + buf * STAGE;
-    char* Bs = As + SA;
-    int kh = 0, kw = 0, c0 = k0, boff = k0;
-    if (MODE != kGemm) {
-      const int tap = k0 >> g.log2SC;
-      c0 = k0 & (g.SC - 1);
-      if (MODE == kDgradS2) {
-        const int th = ntx == 2 ? tap >> 1 : tap, tw = tap - th * ntx;
-        kh = kh0 + 2 * th;
-        kw = kw0 + 2 * tw;
-        boff = (kh * g.KW + kw) * g.SC + c0;
-      } else {
-        kh = tap / g.KW;
-        kw = tap - kh * g.KW;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < B_INS; ++j)
-      glds16(b_src[j] ? (const void*)(b_src[j] + boff) : (const void*)zp, Bs + (j * 32 + wave * 8) * 128);
+  // The K loop walks filter taps in order; inside a tap the 64-deep slices are
+  // contiguous channels.  Row source pointers (and their validity: padding, rows
+  // past M, stride-2 holes) change only at a tap boundary, so they are rebuilt
+  // there (uniform branch) and each K-step only adds the channel offset c0 --
+  // the per-step address arithmetic that made these kernels issue-bound at one
+  // workgroup per CU.  issue() is called with consecutive kt.
+  const int tap_len = MODE == kGemm ? g.Kpad : g.SC;
+  int c0 = 0, kh = kh0, kw = kw0, tw = 0, tap_koff = MODE == kDgradS2 ? (kh0 * g.KW + kw0) * g.SC : 0;
+  const bf16* a_base[A_INS];
+  unsigned a_mask[A_INS];
+  auto set_tap = [&]() {
 #pragma unroll
     for (int i = 0; i < A_INS; ++i) {
-      const void* p = zp;
+      bool ok = a_ok[i];
+      int64_t off = 0;
       if (MODE == kGemm) {
-        if (a_ok[i]) p = src + (int64_t)a_pix[i] * g.K + k0 + a_ck[i];
+        off = (int64_t)a_pix[i] * g.K;
       } else {
         int sy, sx;
-        bool ok = a_ok[i];
         if (MODE == kFwd) {
           sy = a_y[i] + kh; sx = a_x[i] + kw;
         } else if (MODE == kDgradS2) {
@@ -500,9 +520,34 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
           else { sy = ty; sx = tx; }
         }
         ok = ok && (unsigned)sy < (unsigned)g.SH && (unsigned)sx < (unsigned)g.SW;
-        if (ok) p = src + ((int64_t)(a_pix[i] + sy * g.SW + sx) << g.log2SC) + c0 + a_ck[i];
+        off = (int64_t)(a_pix[i] + sy * g.SW + sx) << g.log2SC;
       }
-      glds16(p, As + (i * 32 + wave * 8) * 128);
+      a_base[i] = ok ? src + off + a_ck[i] : reinterpret_cast<const bf16*>(zp);
+      a_mask[i] = ok ? ~0u : 0u;
+    }
+  };
+
+  auto issue = [&](int kt, int buf) {
+    (void)kt;
+    char* As = smem + buf * STAGE;
+    char* Bs = As + SA;
+    if (c0 == 0) set_tap();
+    const unsigned boff = (unsigned)(tap_koff + c0);
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j) glds16(b_base[j] + (boff & b_mask[j]), Bs + (j * 32 + wave * 8) * 128);
+#pragma unroll
+    for (int i = 0; i < A_INS; ++i) glds16(a_base[i] + ((unsigned)c0 & a_mask[i]), As + (i * 32 + wave * 8) * 128);
+    c0 += 64;
+    if (c0 == tap_len) {
+      c0 = 0;
+      if (MODE == kDgradS2) {
+        kw += 2;
+        if (++tw == ntx) { tw = 0; kw = kw0; kh += 2; }
+        tap_koff = (kh * g.KW + kw) * g.SC;
+      } else {
+        if (++kw == g.KW) { kw = 0; ++kh; }
+        tap_koff += g.SC;
+      }
     }
   };
 
@@ -531,6 +576,28 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
   const unsigned ring_base = lds_addr(smem);
   auto compute = [&](int buf) {
     const unsigned slot = ring_base + buf * STAGE;
+    if constexpr (TM + TN == 4 && kPairedFrags) {
+      unsigned addr[2][4];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) addr[kk][r] = slot + frag_off[kk][r];
+      u32x4 f[2][4];
+      lds_issue_frags8(f, addr);
+      lds_wait_first(f[0]);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        if (kk == 1) lds_wait_all(f[1]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f[kk][i]),
+                                                                __builtin_bit_cast(bf16x8, f[kk][TM + j]), acc[i][j],
+                                                                0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       unsigned addr[TM + TN];

@@ -1,0 +1,45 @@
+"""Run ONE conv pass of one shape a few times (PMC counter passes on a single kernel).
+usage: python tools/conv_one.py H W Cin Cout k s p [fwd|dgrad|bwd] [reps]"""
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "6d-pose-estimation_amd")]
+
+from pose6d._lib import call, query, stream  # noqa: E402
+from pose6d.trunk import DTYPES, pack_single  # noqa: E402
+
+
+def main():
+    H, W, Cin, Cout, k, s, p = (int(v) for v in sys.argv[1:8])
+    ps = sys.argv[8] if len(sys.argv) > 8 else "fwd"
+    reps = int(sys.argv[9]) if len(sys.argv) > 9 else 5
+    B, dtype, dev = 32, torch.bfloat16, "cuda"
+    dt = DTYPES[dtype]
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    x = torch.randn(B, H, W, Cin, device=dev).to(dtype)
+    w = torch.randn(Cout, Cin, k, k, device=dev) * 0.05
+    wp, wt = pack_single(w, Cin, dtype)
+    y = torch.empty(B, Ho, Wo, Cout, device=dev, dtype=dtype)
+    dy = torch.randn(B, Ho, Wo, Cout, device=dev).to(dtype)
+    dx = torch.empty(B, H, W, Cin, device=dev, dtype=dtype)
+    stats = torch.empty(query("conv_stats_rows", B, Ho, Wo, Cout), 2, Cout, device=dev)
+    ws = torch.empty(query("conv2d_wgrad_workspace", dt, B, Ho, Wo, Cin, Cout, k, k) // 4 + 1, device=dev)
+    dw = torch.empty(Cout, Cin, k, k, device=dev)
+    st = stream()
+    for _ in range(reps):
+        if ps == "fwd":
+            call("conv2d_fwd", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, st)
+        elif ps == "dgrad":
+            call("conv2d_dgrad", dt, dy, wt, None, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, st)
+        else:
+            call("conv2d_backward_ex", dt, x, dy, wt, None, dx, dw, 0, ws, ws.numel() * 4, B, H, W, Cin, Cin, Cout,
+                 k, k, s, p, Ho, Wo, 1, st)
+    torch.cuda.synchronize()
+    print("done", ps, H, W, Cin, Cout, k, s)
+
+
+if __name__ == "__main__":
+    main()
