@@ -110,7 +110,21 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
     tap_h[s] = tap / g.KW;
     tap_w[s] = tap - tap_h[s] * g.KW;
   }
+  // output-pixel coordinates of this lane's two DMA rows, advanced by 64 pixels per
+  // stage without divisions (issue() is called with consecutive st)
   const int hw = g.RH * g.RW;
+  const int step_y = MS / g.RW, step_x = MS - step_y * g.RW;
+  int rn[2], roy[2], rox[2];
+  if (!pointwise) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = mbeg + i * 32 + wave * 8 + r8;
+      rn[i] = m / hw;
+      const int rem = m - rn[i] * hw;
+      roy[i] = rem / g.RW;
+      rox[i] = rem - roy[i] * g.RW;
+    }
+  }
 
   auto issue = [&](int st, int buf) {
     char* base = smem + buf * STAGE;
@@ -124,14 +138,10 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
         const void* p = ok ? (const void*)(dy + (int64_t)m * g.Cout + co0 + s * 64 + ck[i]) : (const void*)zp;
         glds16(p, base + s * SUB + (i * 32 + wave * 8) * 128);
       }
-      int n = 0, sy = 0, sx = 0;
+      int sy = 0, sx = 0;
       if (!pointwise) {
-        const int mm = ok ? m : 0;
-        n = mm / hw;
-        const int rem = mm - n * hw;
-        const int oy = rem / g.RW;
-        sy = oy * g.stride - g.pad;
-        sx = (rem - oy * g.RW) * g.stride - g.pad;
+        sy = roy[i] * g.stride - g.pad;
+        sx = rox[i] * g.stride - g.pad;
       }
 #pragma unroll
       for (int s = 0; s < XS; ++s) {
@@ -141,9 +151,15 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
         } else {
           const int yy = sy + tap_h[s], xx = sx + tap_w[s];
           if (ok && (unsigned)yy < (unsigned)g.SH && (unsigned)xx < (unsigned)g.SW)
-            p = x + ((((int64_t)n * g.SH + yy) * g.SW + xx) << g.log2SC) + ci0[s] + ck[i];
+            p = x + ((((int64_t)rn[i] * g.SH + yy) * g.SW + xx) << g.log2SC) + ci0[s] + ck[i];
         }
         glds16(p, base + (YS + s) * SUB + (i * 32 + wave * 8) * 128);
+      }
+      if (!pointwise) {
+        rox[i] += step_x;
+        roy[i] += step_y;
+        if (rox[i] >= g.RW) { rox[i] -= g.RW; ++roy[i]; }
+        while (roy[i] >= g.RH) { roy[i] -= g.RH; ++rn[i]; }
       }
     }
   };
