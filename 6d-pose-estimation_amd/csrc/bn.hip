@@ -73,8 +73,8 @@ __global__ __launch_bounds__(kThreads) void bn_stats_stage1_kernel(const float* 
   if (c < C) {
     int r = r0 + ln;
     for (; r + 16 < r1; r += 32) {
-      const float s0 = part[(int64_t)r * 2 * C + c], q0 = part[(int64_t)r * 2 * C + C + c];
-      const float s1 = part[(int64_t)(r + 16) * 2 * C + c], q1 = part[(int64_t)(r + 16) * 2 * C + C + c];
+      const float s0 = part[(int64_t)c * rows + r], q0 = part[((int64_t)C + c) * rows + r];
+      const float s1 = part[(int64_t)c * rows + r + 16], q1 = part[((int64_t)C + c) * rows + r + 16];
       const double n0 = (double)min((int64_t)32, M - (int64_t)r * 32);
       const double n1 = (double)min((int64_t)32, M - (int64_t)(r + 16) * 32);
       merge(w, n0, (double)s0 / n0, (double)q0);
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(kThreads) void bn_stats_stage1_kernel(const float* 
     }
     if (r < r1) {
       const double nb = (double)min((int64_t)32, M - (int64_t)r * 32);
-      merge(w, nb, (double)part[(int64_t)r * 2 * C + c] / nb, (double)part[(int64_t)r * 2 * C + C + c]);
+      merge(w, nb, (double)part[(int64_t)c * rows + r] / nb, (double)part[((int64_t)C + c) * rows + r]);
     }
   }
   red[0][cl][ln] = w.n;
@@ -117,7 +117,9 @@ __global__ __launch_bounds__(kThreads) void bn_stats_finalize_kernel(
   const int c = blockIdx.x * (kThreads / L) + threadIdx.x / L;
   double s1 = 0.0, s2 = 0.0, K = 0.0;
   if (c < C) {
-    K = (double)part[c] / (double)min((int64_t)32, M);
+    const float* ps = part + (int64_t)c * rows;          // channel-major partials: coalesced rows
+    const float* pq = part + ((int64_t)C + c) * rows;
+    K = (double)ps[0] / (double)min((int64_t)32, M);
     const double n_last = (double)(M - (int64_t)(rows - 1) * 32), inv_last = 1.0 / n_last;
     constexpr int U = 4;
     int r = lane;
@@ -125,8 +127,8 @@ __global__ __launch_bounds__(kThreads) void bn_stats_finalize_kernel(
       float sv[U], qv[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        sv[u] = part[(int64_t)(r + u * L) * 2 * C + c];
-        qv[u] = part[(int64_t)(r + u * L) * 2 * C + C + c];
+        sv[u] = ps[r + u * L];
+        qv[u] = pq[r + u * L];
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -140,9 +142,9 @@ __global__ __launch_bounds__(kThreads) void bn_stats_finalize_kernel(
     for (; r < rows; r += L) {
       const bool last = r == rows - 1;
       const double n = last ? n_last : 32.0, inv_n = last ? inv_last : 0.03125;
-      const double d = (double)part[(int64_t)r * 2 * C + c] - n * K;
+      const double d = (double)ps[r] - n * K;
       s1 += d;
-      s2 += (double)part[(int64_t)r * 2 * C + C + c] + d * d * inv_n;
+      s2 += (double)pq[r] + d * d * inv_n;
     }
   }
   s1 = p6::wave_sum(s1);

@@ -84,7 +84,8 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], ch
     }
   }
   if (stats) {
-    // partials over blocks of 32 rows (two 16-row MFMA tiles), stats row = m / 32:
+    // partials over blocks of 32 rows (two 16-row MFMA tiles), stats row r = m / 32,
+    // stored channel-major: stats[c][r] (sum), stats[C + c][r] (M2):
     // (sum, M2 about the block-local mean) -- Chan-mergeable, free of the
     // E[x^2]-E[x]^2 cancellation; row counts follow from M (pose6d_bn_finalize).
 #pragma unroll
@@ -118,9 +119,10 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], ch
         q += __shfl_xor(q, 32, 64);
         const int c = col_base + j * 16 + fr;
         if (lane < 16 && c < g.Ncols && nval > 0) {
-          float* sp = stats + (int64_t)(rb >> 5) * 2 * g.Ncols;
-          sp[c] = s;
-          sp[g.Ncols + c] = q;
+          // channel-major [2][C][rows]: the finalize reads each channel's rows coalesced
+          const int64_t rows = (g.M + 31) >> 5;
+          stats[(int64_t)c * rows + (rb >> 5)] = s;
+          stats[((int64_t)g.Ncols + c) * rows + (rb >> 5)] = q;
         }
       }
     }

@@ -336,10 +336,10 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC) {
   } else {
     p.bm = Cout >= 128 ? 128 : 64;
     p.bn = Kpad >= 128 ? 128 : 64;
-    target = 1024;
+    target = env_int("POSE6D_WGRAD_BASE_BLOCKS", 1024);
     min_rows = 256;
     step = MT;
-    max_bytes = 16ll << 20;
+    max_bytes = (int64_t)env_int("POSE6D_WGRAD_BASE_MB", 64) << 20;   // stem: 16 -> 64 MiB of slabs, 90 -> 65 us
   }
   const int tiles = p6::ceil_div(Cout, p.bm) * p6::ceil_div(Kpad, p.bn);
   // aim for ~`target` workgroups, each reducing >= min_rows pixels, slabs capped in bytes

@@ -183,7 +183,7 @@ class TrunkEngine:
                 op.wt = e(op.cin_pad, op.k, op.k, op.cout) if op.needs_dgrad else None
                 rows = query("conv_stats_rows", B, op.Ho, op.Wo, op.cout)
                 op.stats_rows = rows
-                op.stats = f32(rows, 2, op.cout)
+                op.stats = f32(2, op.cout, rows)   # channel-major BN partials
                 op.scale, op.shift, op.mean, op.inv = (f32(op.cout) for _ in range(4))
                 ws_w = max(ws_w, query("conv2d_wgrad_workspace", self.dt, B, op.Ho, op.Wo, op.cin_pad, op.cout, op.k,
                                        op.k))

@@ -148,8 +148,10 @@ int pose6d_pack_conv_weights(int32_t dtype, const void *descs, int32_t n_desc, i
 
 /* nn.Conv2d forward (implicit GEMM on MFMA).  x [N][H][W][Cin] (Cin = 4 for the
  * padded stem, else a power of two), wp packed [Cout][Kpad], y [N][Ho][Wo][Cout].
- * bias may be NULL.  stats (NULL = none) receives per-wave BatchNorm partial sums:
- * pose6d_conv_stats_rows(...) rows of [2][Cout] fp32 (sum, sum of squares). */
+ * bias may be NULL.  stats (NULL = none) receives BatchNorm partials over blocks of
+ * 32 output pixels, rows = pose6d_conv_stats_rows(...), stored channel-major
+ * [2][Cout][rows] fp32: stats[c][r] = sum, stats[Cout + c][r] = M2 about the block
+ * mean. */
 int pose6d_conv_stats_rows(int32_t N, int32_t Ho, int32_t Wo, int32_t Cout);
 int pose6d_conv2d_fwd(int32_t dtype, const void *x, const void *wp, const float *bias, void *y, float *stats,
                       int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW,
@@ -202,8 +204,8 @@ int pose6d_bwd_variant(int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t C
 /* nn.BatchNorm2d: finalize the conv-epilogue statistics (training) or use the
  * running statistics (eval) -> scale/shift (+ saved mean / invstd); running
  * stats, num_batches_tracked updated in training (torch semantics).
- * partial: `rows` = ceil(count / 32) rows of [2][C] (sum, M2 about the row's mean)
- * over 32-pixel blocks, folded in fp64 as shifted sums about the first row's
+ * partial: [2][C][rows] (rows = ceil(count / 32); sum, M2 about the block's mean)
+ * over 32-pixel blocks, as pose6d_conv2d_fwd writes them, folded in fp64 as shifted sums about the first row's
  * mean in ONE launch (env POSE6D_BN_TWO_STAGE: the earlier two-launch Chan
  * merge); workspace: 64 * 3 * C doubles (used by the two-stage form only). */
 int pose6d_bn_finalize(const float *partial, int32_t rows, int32_t C, int64_t count, const float *gamma,

@@ -59,7 +59,7 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
     wp, wt = pack_single(wd, cpad, dtype, with_t=Cin >= 8)
     y = torch.empty(N, Ho, Wo, Cout, device=dev, dtype=dtype)
     rows = query("conv_stats_rows", N, Ho, Wo, Cout)
-    stats = torch.empty(rows, 2, Cout, device=dev)
+    stats = torch.empty(2, Cout, rows, device=dev)
     call("conv2d_fwd", dt, xd, wp, b.to(dev) if b is not None else None, y, stats, N, H, W, cpad, Cout, k, k, s, p,
          Ho, Wo, stream())
     xr = x.clone().requires_grad_(True)
@@ -200,14 +200,15 @@ def test_bn_act_and_backward(dtype, C, N, H):
     gamma = torch.rand(C, generator=g) + 0.5
     beta = torch.randn(C, generator=g)
     dev, dt = "cuda", DTYPES[dtype]
-    # statistics partials as the conv epilogue emits them: per 32 pixels (sum, M2)
+    # statistics partials as the conv epilogue emits them: per 32 pixels (sum, M2),
+    # channel-major [2][C][rows]
     flat = y.permute(0, 2, 3, 1).reshape(M, C).double()
     rows = (M + 31) // 32
-    part = torch.zeros(rows, 2, C, dtype=torch.float64)
+    part = torch.zeros(2, C, rows, dtype=torch.float64)
     for r in range(rows):
         blk = flat[32 * r:32 * r + 32]
-        part[r, 0] = blk.sum(0)
-        part[r, 1] = ((blk - blk.mean(0)) ** 2).sum(0)
+        part[0, :, r] = blk.sum(0)
+        part[1, :, r] = ((blk - blk.mean(0)) ** 2).sum(0)
     stats = part.float().to(dev)
     rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
     nbt = torch.zeros((), dtype=torch.long, device=dev)
