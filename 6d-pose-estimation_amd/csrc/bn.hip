@@ -360,9 +360,13 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce2_kernel(const T* __res
 #pragma unroll
       for (int e = 0; e < E; ++e) { s[e] += sred[t][e]; q[e] += sred[t][E + e]; }
     }
-    float* pp = part + (int64_t)blockIdx.y * 2 * C;
+    // channel-major partials [2][C][row blocks] (coalesced reads in the finalize)
+    const int64_t nrb = gridDim.y;
 #pragma unroll
-    for (int e = 0; e < E; ++e) { pp[c0 + e] = s[e]; pp[C + c0 + e] = q[e]; }
+    for (int e = 0; e < E; ++e) {
+      part[(int64_t)(c0 + e) * nrb + blockIdx.y] = s[e];
+      part[((int64_t)C + c0 + e) * nrb + blockIdx.y] = q[e];
+    }
   }
 }
 
@@ -371,31 +375,27 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_finalize_kernel(const float* 
                                                                    const float* __restrict__ inv,
                                                                    float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                                    int accumulate, float* __restrict__ coef) {
-  // block = 16 channels x 16 lanes (4 independent loads in flight per lane)
-  __shared__ double red[2][16][17];
-  const int cl = threadIdx.x & 15, ln = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
+  // one wave per channel: lanes read the channel's partial rows coalesced
+  // (channel-major [2][C][rows]), fp64 sums combined by a fixed xor tree
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  if (c >= C) return;
+  const float* ps = part + (int64_t)c * rows;
+  const float* pq = part + ((int64_t)C + c) * rows;
   double s = 0.0, q = 0.0;
-  if (c < C) {
-    int r = ln;
-    for (; r + 48 < rows; r += 64) {
-      const float* p = part + (int64_t)r * 2 * C + c;
-      const int64_t st = (int64_t)16 * 2 * C;
-      const float s0 = p[0], s1 = p[st], s2 = p[2 * st], s3 = p[3 * st];
-      const float q0 = p[C], q1 = p[st + C], q2 = p[2 * st + C], q3 = p[3 * st + C];
-      s += ((double)s0 + s1) + ((double)s2 + s3);
-      q += ((double)q0 + q1) + ((double)q2 + q3);
-    }
-    for (; r < rows; r += 16) {
-      s += (double)part[(int64_t)r * 2 * C + c];
-      q += (double)part[(int64_t)r * 2 * C + C + c];
-    }
+  int r = lane;
+  for (; r + 64 < rows; r += 128) {
+    const float s0 = ps[r], s1 = ps[r + 64], q0 = pq[r], q1 = pq[r + 64];
+    s += (double)s0 + (double)s1;
+    q += (double)q0 + (double)q1;
   }
-  red[0][cl][ln] = s;
-  red[1][cl][ln] = q;
-  __syncthreads();
-  if (ln == 0 && c < C) {
-    for (int k = 1; k < 16; ++k) { s += red[0][cl][k]; q += red[1][cl][k]; }
+  for (; r < rows; r += 64) {
+    s += (double)ps[r];
+    q += (double)pq[r];
+  }
+  s = p6::wave_sum(s);
+  q = p6::wave_sum(q);
+  if (lane == 0) {
     if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)s;
     if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)q;
     coef[c] = gamma[c] * inv[c];            // c1
@@ -545,7 +545,7 @@ extern "C" int pose6d_bn_bwd(int32_t dtype, const void* dout, const void* out, c
   if (dtype == POSE6D_DT_BF16) reduce((bf16*)nullptr);
   else reduce((float*)nullptr);
   P6_LAUNCH_CHECK();
-  bn_bwd_finalize_kernel<<<p6::ceil_div(C, 16), kThreads, 0, s>>>(part, nb, C, (double)M, gamma, invstd, dgamma, dbeta,
+  bn_bwd_finalize_kernel<<<p6::ceil_div(C, kThreads / 64), kThreads, 0, s>>>(part, nb, C, (double)M, gamma, invstd, dgamma, dbeta,
                                                                   accumulate, coef);
   P6_LAUNCH_CHECK();
   auto apply = [&](auto* typed) {
