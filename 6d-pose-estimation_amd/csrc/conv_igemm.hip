@@ -46,6 +46,22 @@ struct Geom {
   int nmajor;              // fast path: tile order N-major (weights larger than the gathered source)
 };
 
+// BatchNorm backward partials produced by a data-gradient epilogue (bf16 fast path):
+// the dX tile IS the dout of the BN that produced this conv's input, so the
+// epilogue also sums dz = dout * relu_mask and dz * xhat over its 64 rows
+// (pose6d_conv2d_backward_bn; the standalone bn_bwd reduce pass disappears).
+struct BnBwd {
+  const bf16* y;       // that BN's input (the previous conv's raw output), NHWC like dX
+  const bf16* out;     // mk 1: the forward output (mask = out > 0)
+  const float* rs;     // mk 2: mask = bf16(y * rs + rb) > 0 (ReLU recomputed)
+  const float* rb;
+  const float* mean;
+  const float* inv;
+  float* part;         // [2][C][rows] channel-major (sum dz, sum dz * xhat); null = off
+  int rows;
+  int mk;
+};
+
 // ds_read_b128 fragment reads: lanes (row = l & 15, chunk = l >> 4) of a 16-row
 // block; this XOR makes every 16-lane LDS group hit 16 distinct 16-byte slots.
 __device__ __forceinline__ int swz(int row) { return (4 - ((row >> 2) & 3)) & 3; }
@@ -62,14 +78,34 @@ __device__ __forceinline__ int64_t out_row(const Geom& g, int cls, int m) {
 
 // Shared epilogue: + bias, BatchNorm partial statistics, LDS-staged 16-B stores
 // (+ residual).  Must be entered after a barrier that ends all LDS reads.
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, bool BNF = false>
 __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const Geom& g,
                                               const float* __restrict__ bias, const T* __restrict__ res,
                                               T* __restrict__ out, float* __restrict__ stats, int m0, int n0,
-                                              int cls = -1) {
+                                              int cls = -1, const BnBwd* bn = nullptr, int prow = 0) {
   constexpr int TM = BM / 32, TN = BN / 32;
   constexpr int CROW = BN * (int)sizeof(T) + 16;  // epilogue tile row stride (bytes)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // BN-backward epilogue: the BN's y (and forward output) chunks this thread will
+  // need in the store loop are fetched first, so their latency overlaps the
+  // staging below instead of serialising behind each store
+  constexpr int kBnIt = (BM * (BN * (int)sizeof(T) / 16) + kThreads - 1) / kThreads;
+  uint4 pre_y[BNF ? kBnIt : 1], pre_o[BNF ? kBnIt : 1];
+  if constexpr (BNF) {
+    constexpr int CPR0 = BN * (int)sizeof(T) / 16;
+#pragma unroll
+    for (int it = 0; it < kBnIt; ++it) {
+      const int idx = tid + it * kThreads;
+      const int lr = idx / CPR0, cc = idx - lr * CPR0;
+      const int m = m0 + lr, c = n0 + cc * (16 / (int)sizeof(T));
+      pre_y[it] = pre_o[it] = uint4{0, 0, 0, 0};
+      if (idx < BM * CPR0 && m < g.M && c < g.Ncols) {
+        const int64_t om = out_row(g, cls, m);
+        pre_y[it] = *reinterpret_cast<const uint4*>(bn->y + om * g.Ncols + c);
+        if (bn->mk == 1) pre_o[it] = *reinterpret_cast<const uint4*>(bn->out + om * g.Ncols + c);
+      }
+    }
+  }
   const int wm = wave >> 1, wn = wave & 1;
   const int fr = lane & 15, fc = lane >> 4;
   const int row_base = m0 + wm * (BM / 2);
@@ -140,16 +176,25 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], ch
       }
   __syncthreads();
   constexpr int CPR = BN * (int)sizeof(T) / 16;  // 16-B chunks per tile row
-  for (int idx = tid; idx < BM * CPR; idx += kThreads) {
+  constexpr int E = 16 / (int)sizeof(T);
+  constexpr bool kBnOk = BNF && sizeof(T) == 2 && CPR == 8 && kThreads % CPR == 0;
+  static_assert(!BNF || kBnOk, "BN-backward epilogue: bf16 64-column tiles only");
+  const bool bnf = kBnOk;
+  float bs[E], bq[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) bs[e] = bq[e] = 0.f;
+#pragma unroll
+  for (int it = 0; it < (BM * CPR + kThreads - 1) / kThreads; ++it) {
+    const int idx = tid + it * kThreads;
+    if (idx >= BM * CPR) break;
     const int lr = idx / CPR, cc = idx - lr * CPR;
-    const int m = m0 + lr, c = n0 + cc * (16 / (int)sizeof(T));
+    const int m = m0 + lr, c = n0 + cc * E;
     if (m >= g.M || c >= g.Ncols) continue;
     uint4 v = *reinterpret_cast<const uint4*>(smem + lr * CROW + cc * 16);
     const int64_t om = out_row(g, cls, m);
     T* dst = out + om * g.Ncols + c;
     if (res) {
       const uint4 rv = *reinterpret_cast<const uint4*>(res + om * g.Ncols + c);
-      constexpr int E = 16 / (int)sizeof(T);
       T a[E], b[E];
       __builtin_memcpy(a, &v, 16);
       __builtin_memcpy(b, &rv, 16);
@@ -158,6 +203,62 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], ch
       __builtin_memcpy(&v, a, 16);
     }
     *reinterpret_cast<uint4*>(dst) = v;
+    if constexpr (kBnOk) {
+      if (bnf) {
+        // dout = v (as stored); dz = dout * mask; sums of dz and dz * xhat (bn_bwd_reduce2 semantics)
+        T a[E], yv[E], ov[E];
+        __builtin_memcpy(a, &v, 16);
+        __builtin_memcpy(yv, &pre_y[it], 16);
+        __builtin_memcpy(ov, &pre_o[it], 16);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const float yy = p6::to_f(yv[e]);
+          bool keep = true;
+          if (bn->mk == 1) keep = p6::to_f(ov[e]) > 0.f;
+          else if (bn->mk == 2) keep = p6::to_f(p6::from_f<T>(fmaf(yy, bn->rs[c + e], bn->rb[c + e]))) > 0.f;
+          const float d = keep ? p6::to_f(a[e]) : 0.f;
+          bs[e] += d;
+          bq[e] = fmaf(d, (yy - bn->mean[c + e]) * bn->inv[c + e], bq[e]);
+        }
+      }
+    }
+  }
+  if constexpr (kBnOk) {
+    if (bnf) {
+      // lanes with the same chunk column: tid % 8 -> fold lane bits 3..5, then 4 waves in LDS
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+#pragma unroll
+        for (int o = 8; o < 64; o <<= 1) {
+          bs[e] += __shfl_xor(bs[e], o, 64);
+          bq[e] += __shfl_xor(bq[e], o, 64);
+        }
+      }
+      __syncthreads();   // every staging read is done: reuse the tile buffer
+      float* red = reinterpret_cast<float*>(smem);   // [waves][8 chunks][2][8]
+      const int wv = tid >> 6;
+      if (lane < CPR) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          red[((wv * CPR + lane) * 2 + 0) * E + e] = bs[e];
+          red[((wv * CPR + lane) * 2 + 1) * E + e] = bq[e];
+        }
+      }
+      __syncthreads();
+      if (tid < BN) {
+        const int cc = tid / E, e = tid - cc * E, c = n0 + tid;
+        float s = 0.f, q = 0.f;
+#pragma unroll
+        for (int w = 0; w < kThreads / 64; ++w) {
+          s += red[((w * CPR + cc) * 2 + 0) * E + e];
+          q += red[((w * CPR + cc) * 2 + 1) * E + e];
+        }
+        if (c < g.Ncols) {
+          bn->part[(int64_t)c * bn->rows + prow] = s;
+          bn->part[((int64_t)g.Ncols + c) * bn->rows + prow] = q;
+        }
+      }
+    }
   }
 }
 
@@ -414,11 +515,12 @@ constexpr bool kPairedFrags = POSE6D_PAIRED_FRAGS;
 
 // one workgroup's work; `bid_in` = its index in this conv's sub-grid (the whole grid,
 // or the leading part of a fused backward launch), `smem` = the kernel's dynamic LDS
-template <int BM, int BN, int MODE, int S>
+template <int BM, int BN, int MODE, int S, bool BNF = false>
 __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16* __restrict__ src,
                                               const bf16* __restrict__ wts, const float* __restrict__ bias,
                                               const bf16* __restrict__ res, bf16* __restrict__ out,
-                                              float* __restrict__ stats, const Geom& g) {
+                                              float* __restrict__ stats, const Geom& g,
+                                              const BnBwd* bn = nullptr) {
   constexpr int TM = BM / 32, TN = BN / 32;
   constexpr int A_INS = BM / 32, B_INS = BN / 32;   // DMA instructions per thread per stage
   constexpr int LOADS = A_INS + B_INS;
@@ -629,7 +731,8 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
     wbuf = wbuf == S - 1 ? 0 : wbuf + 1;
   }
   asm volatile("s_barrier" ::: "memory");   // every wave done reading the ring before the epilogue reuses it
-  conv_epilogue<bf16, BM, BN>(acc, smem, g, bias, res, out, stats, m0, n0, cls);
+  conv_epilogue<bf16, BM, BN, BNF>(acc, smem, g, bias, res, out, stats, m0, n0, cls, bn,
+                                   MODE == kDgradS2 ? tm * 4 + cls : tm);
 }
 
 template <int BM, int BN, int MODE, int S>
@@ -646,16 +749,16 @@ __global__ __launch_bounds__(kThreads) void conv_lds_kernel(const bf16* __restri
 // each part's XCD remap intact; the padding workgroups exit at once).  Both read
 // the same dY, and the weight-gradient workgroups fill the CUs the (often small)
 // data-gradient grid leaves idle -- one launch instead of two.
-template <int DMODE, int DS, int WS>
+template <int DMODE, int DS, int WS, bool BNF>
 __global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ wt,
                                                             const bf16* __restrict__ dres, bf16* __restrict__ dx,
                                                             Geom gd, int nd, int nd_pad,
                                                             const bf16* __restrict__ x, float* __restrict__ ws,
-                                                            p6::WGeom gw) {
+                                                            p6::WGeom gw, BnBwd bn) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x;
   if (b < nd_pad) {
-    if (b < nd) conv_lds_body<64, 64, DMODE, DS>(smem, b, dy, wt, nullptr, dres, dx, nullptr, gd);
+    if (b < nd) conv_lds_body<64, 64, DMODE, DS, BNF>(smem, b, dy, wt, nullptr, dres, dx, nullptr, gd, &bn);
   } else {
     conv_wgrad_lds_body<64, 64, WS>(smem, b - nd_pad, x, dy, ws, gw);
   }
@@ -930,7 +1033,7 @@ namespace {
 
 template <int DMODE, int DS, int WS>
 int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void* wt, const void* dres, void* dx,
-               const void* x, float* ws, hipStream_t s) {
+               const void* x, float* ws, const BnBwd& bn, hipStream_t s) {
   Geom gd = gd0;
   gd.gm = p6::ceil_div(gd.M, 64);
   gd.gn = p6::ceil_div(gd.Ncols, 64);
@@ -943,18 +1046,21 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
   const int ring_w = WS * 128 * 128;
   int lds = ring_d > epi ? ring_d : epi;
   lds = lds > ring_w ? lds : ring_w;
-  conv_bwd_kernel<DMODE, DS, WS><<<nd_pad + nw, kThreads, lds, s>>>((const bf16*)dy, (const bf16*)wt,
-                                                                    (const bf16*)dres, (bf16*)dx, gd, nd, nd_pad,
-                                                                    (const bf16*)x, ws, gw);
+  if (bn.part)
+    conv_bwd_kernel<DMODE, DS, WS, true><<<nd_pad + nw, kThreads, lds, s>>>(
+        (const bf16*)dy, (const bf16*)wt, (const bf16*)dres, (bf16*)dx, gd, nd, nd_pad, (const bf16*)x, ws, gw, bn);
+  else
+    conv_bwd_kernel<DMODE, DS, WS, false><<<nd_pad + nw, kThreads, lds, s>>>(
+        (const bf16*)dy, (const bf16*)wt, (const bf16*)dres, (bf16*)dx, gd, nd, nd_pad, (const bf16*)x, ws, gw, bn);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
 
 template <int DMODE>
 int launch_bwd_mode(int ds, const Geom& gd, const p6::WGeom& gw, const void* dy, const void* wt, const void* dres,
-                    void* dx, const void* x, float* ws, hipStream_t s) {
-  return ds == 2 ? launch_bwd<DMODE, 2, 3>(gd, gw, dy, wt, dres, dx, x, ws, s)
-                 : launch_bwd<DMODE, 4, 3>(gd, gw, dy, wt, dres, dx, x, ws, s);
+                    void* dx, const void* x, float* ws, const BnBwd& bn, hipStream_t s) {
+  return ds == 2 ? launch_bwd<DMODE, 2, 3>(gd, gw, dy, wt, dres, dx, x, ws, bn, s)
+                 : launch_bwd<DMODE, 4, 3>(gd, gw, dy, wt, dres, dx, x, ws, bn, s);
 }
 
 }  // namespace
@@ -980,11 +1086,61 @@ extern "C" int pose6d_conv2d_backward(int32_t dtype, const void* x, const void* 
                                    Cin_real, Cout, KH, KW, stride, pad, Ho, Wo, 3, stream);
 }
 
+namespace {
+int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void* wt, const void* dres, void* dx,
+                       float* dw, int32_t accumulate, float* workspace, int64_t ws_bytes, int32_t N, int32_t H,
+                       int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
+                       int32_t pad, int32_t Ho, int32_t Wo, int32_t phases, const BnBwd& bn, void* stream);
+}  // namespace
+
 extern "C" int pose6d_conv2d_backward_ex(int32_t dtype, const void* x, const void* dy, const void* wt,
                                          const void* dres, void* dx, float* dw, int32_t accumulate, float* workspace,
                                          int64_t ws_bytes, int32_t N, int32_t H, int32_t W, int32_t Cin,
                                          int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
                                          int32_t pad, int32_t Ho, int32_t Wo, int32_t phases, void* stream) {
+  return conv_backward_impl(dtype, x, dy, wt, dres, dx, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real,
+                            Cout, KH, KW, stride, pad, Ho, Wo, phases, BnBwd{}, stream);
+}
+
+// partial rows the fused backward's data-gradient epilogue writes for
+// pose6d_conv2d_backward_bn (one per 64-pixel tile, x4 parity classes on the
+// stride-2 path); 0 = this conv does not run the fused LDS-DMA backward
+extern "C" int pose6d_conv2d_bn_rows(int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout,
+                                     int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo) {
+  if (Cin % 8 != 0 || ilog2(Cin) < 3) return 0;
+  int mode;
+  const Geom gd0 = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
+  const Plan pd = choose(dtype, mode, gd0);
+  p6::WgradPlan pw;
+  p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
+  if (!bwd_fused(pd, pw)) return 0;
+  return p6::ceil_div(pd.g.M, 64) * (pd.mode == kDgradS2 ? 4 : 1);
+}
+
+extern "C" int pose6d_conv2d_backward_bn(int32_t dtype, const void* x, const void* dy, const void* wt,
+                                         const void* dres, void* dx, float* dw, int32_t accumulate, float* workspace,
+                                         int64_t ws_bytes, int32_t N, int32_t H, int32_t W, int32_t Cin,
+                                         int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
+                                         int32_t pad, int32_t Ho, int32_t Wo, const void* bn_y, const void* bn_out,
+                                         const float* bn_rs, const float* bn_rb, const float* bn_mean,
+                                         const float* bn_invstd, float* bn_part, int32_t bn_rows, int32_t bn_mk,
+                                         void* stream) {
+  const int rows = pose6d_conv2d_bn_rows(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo);
+  P6_CHECK_ARG(rows > 0 && rows == bn_rows && dx != nullptr,
+               "pose6d_conv2d_backward_bn: not on the fused path or bn_rows %d != %d", bn_rows, rows);
+  P6_CHECK_ARG(bn_y && bn_mean && bn_invstd && bn_part && bn_mk >= 0 && bn_mk <= 2 && (bn_mk != 1 || bn_out) &&
+                   (bn_mk != 2 || (bn_rs && bn_rb)),
+               "pose6d_conv2d_backward_bn: incomplete BatchNorm arguments");
+  BnBwd bn{(const bf16*)bn_y, (const bf16*)bn_out, bn_rs, bn_rb, bn_mean, bn_invstd, bn_part, bn_rows, bn_mk};
+  return conv_backward_impl(dtype, x, dy, wt, dres, dx, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real,
+                            Cout, KH, KW, stride, pad, Ho, Wo, 3, bn, stream);
+}
+
+namespace {
+int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void* wt, const void* dres, void* dx,
+                       float* dw, int32_t accumulate, float* workspace, int64_t ws_bytes, int32_t N, int32_t H,
+                       int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
+                       int32_t pad, int32_t Ho, int32_t Wo, int32_t phases, const BnBwd& bn, void* stream) {
   P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_backward: bad dtype %d", dtype);
   P6_CHECK_ARG(phases >= 1 && phases <= 3, "pose6d_conv2d_backward_ex: phases must be 1, 2 or 3");
   if (dx == nullptr)
@@ -1014,14 +1170,17 @@ extern "C" int pose6d_conv2d_backward_ex(int32_t dtype, const void* x, const voi
   int rc = POSE6D_OK;
   if (phases & 1) {
     switch (pd.mode) {
-      case kGemm: rc = launch_bwd_mode<kGemm>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, s); break;
-      case kDgradS2: rc = launch_bwd_mode<kDgradS2>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, s); break;
-      default: rc = launch_bwd_mode<kDgrad>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, s); break;
+      case kGemm: rc = launch_bwd_mode<kGemm>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, bn, s); break;
+      case kDgradS2:
+        rc = launch_bwd_mode<kDgradS2>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, bn, s);
+        break;
+      default: rc = launch_bwd_mode<kDgrad>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, bn, s); break;
     }
   }
   if (rc || !(phases & 2)) return rc;
   return p6::wgrad_reduce_launch(workspace, dw, Cout, gw.Kpad, Cin, Cin_real, KH, KW, gw.splits, accumulate, s);
 }
+}  // namespace
 
 // launch variant of a forward / data-gradient conv, for profiling joins:
 // (stages << 12) | (fast << 8) | (mode << 4) | tile, tile 0 = 128x128, 1 = 128x64,

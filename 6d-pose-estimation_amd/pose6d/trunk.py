@@ -16,6 +16,7 @@ Only one forward's activations are kept: backward() must follow the forward it
 differentiates (checked with a generation counter).
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -194,6 +195,23 @@ class TrunkEngine:
             elif isinstance(op, _PoolOp):
                 op.argmax = torch.empty(B, o.H, o.W, o.C, device=device, dtype=torch.uint8)
         self.ws_wgrad = f32(max(ws_w // 4, 1))
+        # BN-backward partials from the data-gradient epilogue (opt-in, POSE6D_BN_EPI=1):
+        # the conv whose input is an ActOp's output writes that BN's (sum dz, sum dz *
+        # xhat) per 64-pixel tile and the standalone reduce pass is skipped.  Measured
+        # slower at batch 32 (6.05 vs 5.70 ms/step): the epilogue work sits on the
+        # short, latency-bound data-gradient workgroups -- DESIGN.md, rejected experiments
+        producer = {id(op.out): op for op in self.ops if isinstance(op, _ActOp)}
+        fuse = os.environ.get("POSE6D_BN_EPI", "0") == "1"
+        for op in self.convs:
+            op.bn_act = producer.get(id(op.src)) if (fuse and op.needs_dgrad) else None
+            op.bn_rows = 0
+            if op.bn_act is not None:
+                op.bn_rows = query("conv2d_bn_rows", self.dt, B, op.H, op.W, op.cin_pad, op.cout, op.k, op.k,
+                                   op.stride, op.pad, op.Ho, op.Wo)
+            op.bn_part = f32(2, op.cin_pad, op.bn_rows) if op.bn_rows > 0 else None
+        for op in self.ops:
+            if isinstance(op, _ActOp):
+                op.bn_ready = None
         self.ws_bn = f32(max(ws_bn, 1))
         self.ws_fin = torch.empty(64 * 3 * max(op.cout for op in self.convs), device=device, dtype=torch.float64)
         self.feat = f32(B, self.feat_dim)
@@ -303,8 +321,16 @@ class TrunkEngine:
                 plain = op.relu and op.res_act is None and op.res_conv is None
                 out = op.out.t if (op.relu and not plain) else None
                 rs, rb = (c.scale, c.shift) if plain else (None, None)
-                call("bn_bwd", dt, op.out.g, out, rs, rb, c.out.t, c.mean, c.inv, bn.weight.detach(),
-                     grad_of(bn.weight), grad_of(bn.bias), acc, c.out.g, op.dz, self.ws_bn, M, c.cout, st)
+                if op.bn_ready is not None:
+                    # the partial sums came with the dgrad that produced op.out.g
+                    part, rows = op.bn_ready
+                    op.bn_ready = None
+                    call("bn_bwd_finish", dt, op.out.g, out, rs, rb, c.out.t, c.mean, c.inv, bn.weight.detach(),
+                         grad_of(bn.weight), grad_of(bn.bias), acc, c.out.g, op.dz, part, rows, self.ws_bn, M,
+                         c.cout, st)
+                else:
+                    call("bn_bwd", dt, op.out.g, out, rs, rb, c.out.t, c.mean, c.inv, bn.weight.detach(),
+                         grad_of(bn.weight), grad_of(bn.bias), acc, c.out.g, op.dz, self.ws_bn, M, c.cout, st)
                 if op.res_conv is not None:
                     r = op.res_conv
                     # identity branch = bn_r(y_r) (no ReLU of its own): its dz is the masked dout
@@ -329,9 +355,21 @@ class TrunkEngine:
                     else:
                         dx = src.g
                 # data + weight gradient: one fused launch on the bf16 fast path
-                call("conv2d_backward", dt, op.src.t, dy, op.wt, dres, dx, grad_of(op.conv.weight), acc,
-                     self.ws_wgrad, self.ws_wgrad.numel() * 4, B, op.H, op.W, op.cin_pad, op.cin, op.cout, op.k,
-                     op.k, op.stride, op.pad, op.Ho, op.Wo, st)
+                args = (dt, op.src.t, dy, op.wt, dres, dx, grad_of(op.conv.weight), acc, self.ws_wgrad,
+                        self.ws_wgrad.numel() * 4, B, op.H, op.W, op.cin_pad, op.cin, op.cout, op.k, op.k,
+                        op.stride, op.pad, op.Ho, op.Wo)
+                a = op.bn_act
+                if a is not None and op.bn_rows > 0 and dx is op.src.g:
+                    # dx is the final dout of BN `a`: its partial sums come out of this epilogue
+                    ac = a.cop
+                    plain_a = a.relu and a.res_act is None and a.res_conv is None
+                    mk = 2 if plain_a else (1 if a.relu else 0)
+                    call("conv2d_backward_bn", *args, ac.out.t, a.out.t if mk == 1 else None,
+                         ac.scale if mk == 2 else None, ac.shift if mk == 2 else None, ac.mean, ac.inv,
+                         op.bn_part, op.bn_rows, mk, st)
+                    a.bn_ready = (op.bn_part, op.bn_rows)
+                else:
+                    call("conv2d_backward", *args, st)
                 if op.conv.bias is not None:
                     call("channel_sum", dt, dy, M, op.cout, grad_of(op.conv.bias), acc, st)
                 if on_conv_done is not None:

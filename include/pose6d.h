@@ -196,6 +196,21 @@ int pose6d_conv2d_backward_ex(int32_t dtype, const void *x, const void *dy, cons
                               int32_t H, int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH,
                               int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, int32_t phases,
                               void *stream);
+/* pose6d_conv2d_backward (all phases) whose data-gradient epilogue ALSO produces the
+ * BatchNorm-backward partials of the BN that made this conv's input x: dX is that
+ * BN's dout, so per 64-pixel tile it writes (sum dz, sum dz * xhat), dz = dout *
+ * mask (bn_mk 0: none, 1: out > 0 with bn_out = the BN's forward output, 2:
+ * bf16(y * rs + rb) > 0), xhat = (y - mean) * invstd, y = bn_y (the BN's input),
+ * into bn_part [2][Cin][bn_rows] for pose6d_bn_bwd_finish.  bf16 fused path only:
+ * bn_rows must equal pose6d_conv2d_bn_rows(...) (> 0). */
+int pose6d_conv2d_bn_rows(int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH,
+                          int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo);
+int pose6d_conv2d_backward_bn(int32_t dtype, const void *x, const void *dy, const void *wt, const void *dres,
+                              void *dx, float *dw, int32_t accumulate, float *workspace, int64_t ws_bytes, int32_t N,
+                              int32_t H, int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH,
+                              int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, const void *bn_y,
+                              const void *bn_out, const float *bn_rs, const float *bn_rb, const float *bn_mean,
+                              const float *bn_invstd, float *bn_part, int32_t bn_rows, int32_t bn_mk, void *stream);
 /* (1 << 16) | (data-gradient mode << 4) | ring stages when pose6d_conv2d_backward
  * runs ONE fused conv_bwd_kernel<mode, stages, 3> launch (+ the reduce), else 0 */
 int pose6d_bwd_variant(int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH,
@@ -227,6 +242,14 @@ int pose6d_bn_bwd(int32_t dtype, const void *dout, const void *out, const float 
                   const float *relu_shift, const void *y, const float *mean, const float *invstd, const float *gamma,
                   float *dgamma, float *dbeta, int32_t accumulate, void *dy, void *dz_out, float *workspace,
                   int64_t M, int32_t C, void *stream);
+
+/* The same backward when the (sum dz, sum dz * xhat) partials already exist, as
+ * [2][C][rows] channel-major (pose6d_conv2d_backward_bn wrote them): finalize +
+ * apply only.  workspace: 3 * C floats. */
+int pose6d_bn_bwd_finish(int32_t dtype, const void *dout, const void *out, const float *relu_scale,
+                         const float *relu_shift, const void *y, const float *mean, const float *invstd,
+                         const float *gamma, float *dgamma, float *dbeta, int32_t accumulate, void *dy, void *dz_out,
+                         const float *partial, int32_t rows, float *workspace, int64_t M, int32_t C, void *stream);
 
 /* conv bias gradient: out[c] (+)= sum_m x[m][c] over an NHWC tensor of M pixels */
 int pose6d_channel_sum(int32_t dtype, const void *x, int64_t M, int32_t C, float *out, int32_t accumulate,
