@@ -110,11 +110,12 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, u
                                    int W, int C, int Ho, int Wo, int k, int s, int p) {
   constexpr int E = V<T>::E;
   const int cpr = C / E;
-  const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;  // (output pixel, chunk)
-  if (i >= (int64_t)N * Ho * Wo * cpr) return;
-  const int c0 = (int)(i % cpr) * E;
-  const int64_t pix = i / cpr;
-  const int ox = pix % Wo, oy = (pix / Wo) % Ho, n = pix / ((int64_t)Wo * Ho);
+  // grid (ceil(Wo * cpr / 256), N * Ho): one output row per blockIdx.y
+  const int i = blockIdx.x * kThreads + threadIdx.x;  // (column, chunk) within the row
+  if (i >= Wo * cpr) return;
+  const int n = blockIdx.y / Ho, oy = blockIdx.y - n * Ho;
+  const int ox = i / cpr, c0 = (i - ox * cpr) * E;
+  const int64_t pix = ((int64_t)n * Ho + oy) * Wo + ox;
   float best[E];
   uint8_t bi[E];
 #pragma unroll
@@ -153,11 +154,12 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __re
                                    int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
   constexpr int E = V<T>::E;
   const int cpr = C / E;
-  const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;  // (input pixel, chunk)
-  if (i >= (int64_t)N * H * W * cpr) return;
-  const int c0 = (int)(i % cpr) * E;
-  const int64_t pix = i / cpr;
-  const int ix = pix % W, iy = (pix / W) % H, n = pix / ((int64_t)W * H);
+  // grid (ceil(W * cpr / 256), N * H): one input row per blockIdx.y
+  const int i = blockIdx.x * kThreads + threadIdx.x;  // (column, chunk) within the row
+  if (i >= W * cpr) return;
+  const int n = blockIdx.y / H, iy = blockIdx.y - n * H;
+  const int ix = i / cpr, c0 = (i - ix * cpr) * E;
+  const int64_t pix = ((int64_t)n * H + iy) * W + ix;
   // windows containing (iy, ix): oy*s - p <= iy <= oy*s - p + k - 1
   const int oy0 = max(0, (iy + p - k + s) / s), oy1 = min(Ho - 1, (iy + p) / s);
   const int ox0 = max(0, (ix + p - k + s) / s), ox1 = min(Wo - 1, (ix + p) / s);
@@ -181,25 +183,48 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __re
   st(dx + pix * C + c0, g);
 }
 
+// block = 64 channel chunks (lanes) x 4 pixel groups (waves), grid (chunk groups, N);
+// the four group sums meet in LDS in fixed order
 template <typename T>
-__global__ void avgpool_fwd_kernel(const T* __restrict__ x, float* __restrict__ y, int N, int HW, int C) {
+__global__ __launch_bounds__(kThreads) void avgpool_fwd_kernel(const T* __restrict__ x, float* __restrict__ y, int N,
+                                                               int HW, int C) {
   constexpr int E = V<T>::E;
+  __shared__ float red[4][64][E + 1];
   const int cpr = C / E;
-  const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;
-  if (i >= (int64_t)N * cpr) return;
-  const int64_t n = i / cpr;
-  const int c0 = (int)(i % cpr) * E;
+  const int cl = threadIdx.x & 63, pg = threadIdx.x >> 6;
+  const int ch = blockIdx.x * 64 + cl;
+  const int64_t n = blockIdx.y;
   float s[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) s[e] = 0.f;
-  for (int p = 0; p < HW; ++p) {
-    float v[E];
-    ld(x + (n * HW + p) * C + c0, v);
+  if (ch < cpr) {
+    int p = pg;
+    for (; p + 12 < HW; p += 16) {
+      float v[4][E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) s[e] += v[e];
+      for (int u = 0; u < 4; ++u) ld(x + (n * HW + p + 4 * u) * C + ch * E, v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int e = 0; e < E; ++e) s[e] += v[u][e];
+    }
+    for (; p < HW; p += 4) {
+      float v[E];
+      ld(x + (n * HW + p) * C + ch * E, v);
+#pragma unroll
+      for (int e = 0; e < E; ++e) s[e] += v[e];
+    }
   }
 #pragma unroll
-  for (int e = 0; e < E; ++e) y[n * C + c0 + e] = s[e] / (float)HW;
+  for (int e = 0; e < E; ++e) red[pg][cl][e] = s[e];
+  __syncthreads();
+  if (pg == 0 && ch < cpr) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float t = ((red[0][cl][e] + red[1][cl][e]) + red[2][cl][e]) + red[3][cl][e];
+      y[n * C + ch * E + e] = t / (float)HW;
+    }
+  }
 }
 
 template <typename T>
@@ -261,15 +286,14 @@ extern "C" int pose6d_maxpool_fwd(int32_t dtype, const void* x, void* y, uint8_t
   P6_CHECK_ARG(k * k <= 255, "pose6d_maxpool_fwd: window too large");
   P6_POOL_CHECK(C, dtype);
   hipStream_t st_ = p6::stream_of(stream);
-  if (dtype == POSE6D_DT_BF16) {
-    const int64_t n = (int64_t)N * Ho * Wo * (C / 8);
-    if (n) maxpool_fwd_kernel<bf16><<<blocks(n), kThreads, 0, st_>>>((const bf16*)x, (bf16*)y, argmax, N, H, W, C, Ho,
-                                                                       Wo, k, s, p);
-  } else {
-    const int64_t n = (int64_t)N * Ho * Wo * (C / 4);
-    if (n) maxpool_fwd_kernel<float><<<blocks(n), kThreads, 0, st_>>>((const float*)x, (float*)y, argmax, N, H, W, C, Ho,
-                                                                        Wo, k, s, p);
-  }
+  if ((int64_t)N * Ho * Wo == 0) return POSE6D_OK;
+  const int E = dtype == POSE6D_DT_BF16 ? 8 : 4;
+  const dim3 grid(p6::ceil_div((int64_t)Wo * (C / E), kThreads), N * Ho);
+  if (dtype == POSE6D_DT_BF16)
+    maxpool_fwd_kernel<bf16><<<grid, kThreads, 0, st_>>>((const bf16*)x, (bf16*)y, argmax, N, H, W, C, Ho, Wo, k, s, p);
+  else
+    maxpool_fwd_kernel<float><<<grid, kThreads, 0, st_>>>((const float*)x, (float*)y, argmax, N, H, W, C, Ho, Wo, k, s,
+                                                          p);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
@@ -279,15 +303,15 @@ extern "C" int pose6d_maxpool_bwd(int32_t dtype, const void* dy, const uint8_t* 
                                   void* stream) {
   P6_POOL_CHECK(C, dtype);
   hipStream_t st_ = p6::stream_of(stream);
-  if (dtype == POSE6D_DT_BF16) {
-    const int64_t n = (int64_t)N * H * W * (C / 8);
-    if (n) maxpool_bwd_kernel<bf16><<<blocks(n), kThreads, 0, st_>>>((const bf16*)dy, argmax, (bf16*)dx, N, H, W, C, Ho,
-                                                                       Wo, k, s, p);
-  } else {
-    const int64_t n = (int64_t)N * H * W * (C / 4);
-    if (n) maxpool_bwd_kernel<float><<<blocks(n), kThreads, 0, st_>>>((const float*)dy, argmax, (float*)dx, N, H, W, C,
-                                                                        Ho, Wo, k, s, p);
-  }
+  if ((int64_t)N * H * W == 0) return POSE6D_OK;
+  const int E = dtype == POSE6D_DT_BF16 ? 8 : 4;
+  const dim3 grid(p6::ceil_div((int64_t)W * (C / E), kThreads), N * H);
+  if (dtype == POSE6D_DT_BF16)
+    maxpool_bwd_kernel<bf16><<<grid, kThreads, 0, st_>>>((const bf16*)dy, argmax, (bf16*)dx, N, H, W, C, Ho, Wo, k, s,
+                                                         p);
+  else
+    maxpool_bwd_kernel<float><<<grid, kThreads, 0, st_>>>((const float*)dy, argmax, (float*)dx, N, H, W, C, Ho, Wo, k,
+                                                          s, p);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
@@ -299,8 +323,9 @@ extern "C" int pose6d_avgpool_fwd(int32_t dtype, const void* x, float* y, int32_
   const int E = dtype == POSE6D_DT_BF16 ? 8 : 4;
   const int64_t n = (int64_t)N * (C / E);
   if (n == 0) return POSE6D_OK;
-  if (dtype == POSE6D_DT_BF16) avgpool_fwd_kernel<bf16><<<blocks(n), kThreads, 0, st_>>>((const bf16*)x, y, N, HW, C);
-  else avgpool_fwd_kernel<float><<<blocks(n), kThreads, 0, st_>>>((const float*)x, y, N, HW, C);
+  const dim3 grid(p6::ceil_div(C / E, 64), N);
+  if (dtype == POSE6D_DT_BF16) avgpool_fwd_kernel<bf16><<<grid, kThreads, 0, st_>>>((const bf16*)x, y, N, HW, C);
+  else avgpool_fwd_kernel<float><<<grid, kThreads, 0, st_>>>((const float*)x, y, N, HW, C);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
