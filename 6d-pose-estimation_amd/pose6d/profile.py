@@ -46,7 +46,7 @@ def conv_launches(eng, fused=True):
         if bv:
             # the step's fused data + weight gradient launch (conv2d_backward phase 1;
             # the slab reduce is its own kernel and row in rocprof)
-            sym = f"conv_bwd_kernel<{(bv >> 4) & 15}, {bv & 15}, 3>"
+            sym = f"conv_bwd_kernel<{(bv >> 4) & 15}, {bv & 15}, 3, false>"
             dw = torch.empty_like(op.conv.weight)
 
             def bwd(op=op, dw=dw):

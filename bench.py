@@ -95,6 +95,9 @@ def main():
     ap.add_argument("--no-kernel-profile", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
     ap.add_argument("--no-side", action="store_true", help="skip the configs[1] / configs[3] side measurements")
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="one eager step + the per-kernel roofline replays only (the command whose rocprofv3 "
+                         "--stats summary profiles/*_roofline_stats.csv holds: same launches, same averages)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -116,6 +119,11 @@ def main():
     B = args.batch
     tr = RGBDGeometricTrainer(model, B, dtype=torch.bfloat16, process_group=pg)
     data = synth_batch(B, dev, seed=1000 + rank)   # each rank its own shard
+    if args.roofline_only:
+        tr.step_eager(data)
+        torch.cuda.synchronize()
+        print(json.dumps(kernel_profile(tr, float("nan"), with_forward=False)), flush=True)
+        return
     if not args.eager:
         tr.capture(data)
     for _ in range(args.warmup):
@@ -166,7 +174,7 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def kernel_profile(tr, step_ms):
+def kernel_profile(tr, step_ms, with_forward=True):
     """Dominant kernel (largest total time per step) -> roofline object, plus the
     forward-pass HBM roofline fraction (the north-star's 60 % target)."""
     from pose6d import profile
@@ -177,7 +185,7 @@ def kernel_profile(tr, step_ms):
     achieved = a["flops"] / a["launches"] / avg_t / 1e12
     conv_total_ms = sum(v["time_s"] for v in agg.values()) * 1e3
     # forward-only (training-mode BN) time of the trunk, graph-captured
-    fwd_ms = forward_time(tr)
+    fwd_ms = forward_time(tr) if with_forward else float("nan")
     fwd_gbs = FWD_BYTES_PER_CROP * tr.B / (fwd_ms * 1e-3) / 1e9
     pmc, tsrc = pmc_traffic(sym)
     traffic = round(pmc["hbm_bytes_per_launch"]) if pmc else None

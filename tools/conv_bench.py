@@ -15,6 +15,7 @@ from pose6d.trunk import DTYPES, pack_single  # noqa: E402
 
 # (H, W, Cin, Cout, k, s, p) per distinct ResNet50 conv (input geometry)
 SHAPES = [
+    (224, 224, 4, 64, 7, 2, 3),
     (56, 56, 64, 64, 1, 1, 0), (56, 56, 64, 64, 3, 1, 1), (56, 56, 64, 256, 1, 1, 0), (56, 56, 256, 64, 1, 1, 0),
     (56, 56, 256, 128, 1, 1, 0), (56, 56, 128, 128, 3, 2, 1), (28, 28, 128, 512, 1, 1, 0), (56, 56, 256, 512, 1, 2, 0),
     (28, 28, 512, 128, 1, 1, 0), (28, 28, 128, 128, 3, 1, 1), (28, 28, 512, 256, 1, 1, 0),
@@ -45,11 +46,12 @@ def main():
     ap.add_argument("--stages", default="auto", help="fast-path LDS ring depths to sweep, e.g. auto,2,3,4,6")
     ap.add_argument("--wgrad-env", default="", help="';'-separated K=V[,K=V] settings to sweep for wgrad")
     ap.add_argument("--B", type=int, default=32)
+    ap.add_argument("--only", type=int, default=-1, help="index into SHAPES")
     a = ap.parse_args()
     B, dt, dtype, dev = a.B, DTYPES[torch.bfloat16], torch.bfloat16, "cuda"
     st = stream()
     tot = {}
-    for (H, W, Cin, Cout, k, s, p) in SHAPES:
+    for (H, W, Cin, Cout, k, s, p) in (SHAPES if a.only < 0 else [SHAPES[a.only]]):
         Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         x = torch.randn(B, H, W, Cin, device=dev).to(dtype)
         w = torch.randn(Cout, Cin, k, k, device=dev) * 0.05

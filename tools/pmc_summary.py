@@ -33,8 +33,11 @@ def _itanium_template(name):
     args, rest = [], rest[1:]
     while rest and not rest.startswith("E"):
         t = re.match(r"Li(-?\d+)E", rest)
+        b = re.match(r"Lb([01])E", rest)
         if t:
             args.append(t.group(1)); rest = rest[t.end():]
+        elif b:
+            args.append("true" if b.group(1) == "1" else "false"); rest = rest[b.end():]
         elif rest.startswith("DF16b"):
             args.append("__bf16"); rest = rest[5:]
         elif rest.startswith("f"):
