@@ -754,13 +754,18 @@ __global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const bf16* __restri
                                                             const bf16* __restrict__ dres, bf16* __restrict__ dx,
                                                             Geom gd, int nd, int nd_pad,
                                                             const bf16* __restrict__ x, float* __restrict__ ws,
-                                                            p6::WGeom gw, BnBwd bn) {
+                                                            p6::WGeom gw, BnBwd bn, ReduceJob rj) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x;
+  const int nw = gw.gm * gw.gn * gw.splits;
   if (b < nd_pad) {
     if (b < nd) conv_lds_body<64, 64, DMODE, DS, BNF>(smem, b, dy, wt, nullptr, dres, dx, nullptr, gd, &bn);
-  } else {
+  } else if (b < nd_pad + nw) {
     conv_wgrad_lds_body<64, 64, WS>(smem, b - nd_pad, x, dy, ws, gw);
+  } else {
+    // the previous conv's weight-gradient slabs (another workspace), reduced here
+    // instead of in a launch of their own
+    run_reduce_job(smem, b - nd_pad - nw, rj);
   }
 }
 
@@ -1033,7 +1038,7 @@ namespace {
 
 template <int DMODE, int DS, int WS>
 int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void* wt, const void* dres, void* dx,
-               const void* x, float* ws, const BnBwd& bn, hipStream_t s) {
+               const void* x, float* ws, const BnBwd& bn, const ReduceJob& rj, hipStream_t s) {
   Geom gd = gd0;
   gd.gm = p6::ceil_div(gd.M, 64);
   gd.gn = p6::ceil_div(gd.Ncols, 64);
@@ -1047,20 +1052,22 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
   int lds = ring_d > epi ? ring_d : epi;
   lds = lds > ring_w ? lds : ring_w;
   if (bn.part)
-    conv_bwd_kernel<DMODE, DS, WS, true><<<nd_pad + nw, kThreads, lds, s>>>(
-        (const bf16*)dy, (const bf16*)wt, (const bf16*)dres, (bf16*)dx, gd, nd, nd_pad, (const bf16*)x, ws, gw, bn);
+    conv_bwd_kernel<DMODE, DS, WS, true><<<nd_pad + nw + rj.nblk, kThreads, lds, s>>>(
+        (const bf16*)dy, (const bf16*)wt, (const bf16*)dres, (bf16*)dx, gd, nd, nd_pad, (const bf16*)x, ws, gw, bn,
+        rj);
   else
-    conv_bwd_kernel<DMODE, DS, WS, false><<<nd_pad + nw, kThreads, lds, s>>>(
-        (const bf16*)dy, (const bf16*)wt, (const bf16*)dres, (bf16*)dx, gd, nd, nd_pad, (const bf16*)x, ws, gw, bn);
+    conv_bwd_kernel<DMODE, DS, WS, false><<<nd_pad + nw + rj.nblk, kThreads, lds, s>>>(
+        (const bf16*)dy, (const bf16*)wt, (const bf16*)dres, (bf16*)dx, gd, nd, nd_pad, (const bf16*)x, ws, gw, bn,
+        rj);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
 
 template <int DMODE>
 int launch_bwd_mode(int ds, const Geom& gd, const p6::WGeom& gw, const void* dy, const void* wt, const void* dres,
-                    void* dx, const void* x, float* ws, const BnBwd& bn, hipStream_t s) {
-  return ds == 2 ? launch_bwd<DMODE, 2, 3>(gd, gw, dy, wt, dres, dx, x, ws, bn, s)
-                 : launch_bwd<DMODE, 4, 3>(gd, gw, dy, wt, dres, dx, x, ws, bn, s);
+                    void* dx, const void* x, float* ws, const BnBwd& bn, const ReduceJob& rj, hipStream_t s) {
+  return ds == 2 ? launch_bwd<DMODE, 2, 3>(gd, gw, dy, wt, dres, dx, x, ws, bn, rj, s)
+                 : launch_bwd<DMODE, 4, 3>(gd, gw, dy, wt, dres, dx, x, ws, bn, rj, s);
 }
 
 }  // namespace
@@ -1090,7 +1097,8 @@ namespace {
 int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void* wt, const void* dres, void* dx,
                        float* dw, int32_t accumulate, float* workspace, int64_t ws_bytes, int32_t N, int32_t H,
                        int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
-                       int32_t pad, int32_t Ho, int32_t Wo, int32_t phases, const BnBwd& bn, void* stream);
+                       int32_t pad, int32_t Ho, int32_t Wo, int32_t phases, const BnBwd& bn, void* stream,
+                       const ReduceJob* rj = nullptr, int32_t* deferred = nullptr);
 }  // namespace
 
 extern "C" int pose6d_conv2d_backward_ex(int32_t dtype, const void* x, const void* dy, const void* wt,
@@ -1140,12 +1148,24 @@ namespace {
 int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void* wt, const void* dres, void* dx,
                        float* dw, int32_t accumulate, float* workspace, int64_t ws_bytes, int32_t N, int32_t H,
                        int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
-                       int32_t pad, int32_t Ho, int32_t Wo, int32_t phases, const BnBwd& bn, void* stream) {
+                       int32_t pad, int32_t Ho, int32_t Wo, int32_t phases, const BnBwd& bn, void* stream,
+                       const ReduceJob* rj, int32_t* deferred) {
   P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_backward: bad dtype %d", dtype);
+  if (deferred) *deferred = 0;
+  const ReduceJob none{};
+  auto flush_prev = [&]() -> int {   // the carried reduce as a launch of its own
+    if (!rj || rj->nblk == 0) return POSE6D_OK;
+    return p6::wgrad_reduce_launch(rj->ws, rj->dw, rj->Cout, rj->Kpad, rj->SC, rj->Cin, rj->KH, rj->KW, rj->splits,
+                                   rj->accumulate, p6::stream_of(stream));
+  };
   P6_CHECK_ARG(phases >= 1 && phases <= 3, "pose6d_conv2d_backward_ex: phases must be 1, 2 or 3");
-  if (dx == nullptr)
-    return !(phases & 1) ? POSE6D_OK : pose6d_conv2d_wgrad(dtype, x, dy, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real, Cout, KH,
+  if (dx == nullptr) {
+    if (!(phases & 1)) return POSE6D_OK;
+    const int rc = flush_prev();
+    if (rc) return rc;
+    return pose6d_conv2d_wgrad(dtype, x, dy, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real, Cout, KH,
                                KW, stride, pad, Ho, Wo, stream);
+  }
   P6_CHECK_ARG(stride == 1 || stride == 2, "pose6d_conv2d_backward: stride must be 1 or 2");
   P6_CHECK_ARG(Cin % 8 == 0 && Cin_real <= Cin && ilog2(Cin) >= 3,
                "pose6d_conv2d_backward: Cin must be a power of two >= 8 for the data gradient");
@@ -1157,8 +1177,9 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
   const bool fused = bwd_fused(pd, pw);
   if (!fused) {
     if (!(phases & 1)) return POSE6D_OK;
-    const int rc = pose6d_conv2d_dgrad(dtype, dy, wt, dres, dx, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo,
-                                       stream);
+    int rc = flush_prev();
+    if (rc) return rc;
+    rc = pose6d_conv2d_dgrad(dtype, dy, wt, dres, dx, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, stream);
     if (rc) return rc;
     return pose6d_conv2d_wgrad(dtype, x, dy, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real, Cout, KH,
                                KW, stride, pad, Ho, Wo, stream);
@@ -1168,14 +1189,23 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
                (long long)pw.splits * Cout * gw.Kpad * 4);
   hipStream_t s = p6::stream_of(stream);
   int rc = POSE6D_OK;
+  const ReduceJob& carried = rj ? *rj : none;
   if (phases & 1) {
     switch (pd.mode) {
-      case kGemm: rc = launch_bwd_mode<kGemm>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, bn, s); break;
-      case kDgradS2:
-        rc = launch_bwd_mode<kDgradS2>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, bn, s);
+      case kGemm:
+        rc = launch_bwd_mode<kGemm>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, bn, carried, s);
         break;
-      default: rc = launch_bwd_mode<kDgrad>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, bn, s); break;
+      case kDgradS2:
+        rc = launch_bwd_mode<kDgradS2>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, bn, carried, s);
+        break;
+      default:
+        rc = launch_bwd_mode<kDgrad>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, bn, carried, s);
+        break;
     }
+  }
+  if (deferred) {   // chain mode: this conv's slab reduce rides on the next launch
+    *deferred = rc == POSE6D_OK;
+    return rc;
   }
   if (rc || !(phases & 2)) return rc;
   return p6::wgrad_reduce_launch(workspace, dw, Cout, gw.Kpad, Cin, Cin_real, KH, KW, gw.splits, accumulate, s);
@@ -1206,4 +1236,41 @@ extern "C" int pose6d_bwd_variant(int32_t dtype, int32_t N, int32_t H, int32_t W
   p6::WgradPlan pw;
   p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
   return bwd_fused(pd, pw) ? (1 << 16) | (pd.mode << 4) | pd.stages : 0;
+}
+
+namespace {
+ReduceJob make_job(const pose6d_wgrad_reduce_t& j) {
+  p6::WgradPlan pw;
+  const p6::WGeom g = p6::wgrad_geom(j.dtype, j.N, j.H, j.W, j.Cin, j.Cout, j.KH, j.KW, j.stride, j.pad, j.Ho, j.Wo,
+                                     &pw);
+  ReduceJob r{};
+  r.ws = j.ws; r.dw = j.dw; r.Cout = j.Cout; r.Kpad = g.Kpad; r.SC = j.Cin; r.Cin = j.Cin_real;
+  r.KH = j.KH; r.KW = j.KW; r.splits = g.splits; r.accumulate = j.accumulate;
+  r.G = reduce_group(g.splits);
+  r.nblk = reduce_blocks(j.Cout, g.Kpad, r.G);
+  return r;
+}
+}  // namespace
+
+extern "C" int pose6d_wgrad_reduce(const pose6d_wgrad_reduce_t* job, void* stream) {
+  P6_CHECK_ARG(job != nullptr, "pose6d_wgrad_reduce: null job");
+  const ReduceJob r = make_job(*job);
+  return p6::wgrad_reduce_launch(r.ws, r.dw, r.Cout, r.Kpad, r.SC, r.Cin, r.KH, r.KW, r.splits, r.accumulate,
+                                 p6::stream_of(stream));
+}
+
+extern "C" int pose6d_conv2d_backward_chain(int32_t dtype, const void* x, const void* dy, const void* wt,
+                                            const void* dres, void* dx, float* dw, int32_t accumulate,
+                                            float* workspace, int64_t ws_bytes, int32_t N, int32_t H, int32_t W,
+                                            int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW,
+                                            int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
+                                            const pose6d_wgrad_reduce_t* prev, int32_t* deferred, void* stream) {
+  P6_CHECK_ARG(deferred != nullptr, "pose6d_conv2d_backward_chain: deferred must point to an int32");
+  ReduceJob r{};
+  if (prev) {
+    P6_CHECK_ARG(prev->ws != workspace, "pose6d_conv2d_backward_chain: prev slabs must live in another workspace");
+    r = make_job(*prev);
+  }
+  return conv_backward_impl(dtype, x, dy, wt, dres, dx, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real,
+                            Cout, KH, KW, stride, pad, Ho, Wo, 3, BnBwd{}, stream, prev ? &r : nullptr, deferred);
 }

@@ -241,4 +241,88 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
 }
 
 
+// sum the split slabs (fixed order) into the OIHW fp32 gradient; k = (kh, kw, ci).
+// Block = L float4 lanes (4 consecutive k each) x G split groups: group g sums
+// slabs g, g + G, ... with U loads in flight, then the G partials are combined in
+// LDS in group order (deterministic).  G is picked so that small gradients with
+// hundreds of splits still spread their reads over many lanes.  `blk` = this
+// workgroup's index among the reduce's workgroups; `red` = 256 float4 of LDS.
+template <int G>
+__device__ __forceinline__ void wgrad_reduce_body(float4* red, int blk, const float* __restrict__ ws,
+                                                  float* __restrict__ dw, int Cout, int Kpad, int SC, int Cin, int KH,
+                                                  int KW, int splits, int accumulate) {
+  constexpr int L = 256 / G;
+  constexpr int U = 4;
+  const int lane = threadIdx.x % L, grp = threadIdx.x / L;
+  const int64_t e0 = ((int64_t)blk * L + lane) * 4;   // first of 4 consecutive (co, k) elements
+  const int64_t total = (int64_t)Cout * Kpad;
+  const bool ok = e0 < total;
+  const int64_t slab = total;
+  float4 acc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ok) {
+    const float* p = ws + e0;
+    int i = grp;
+    for (; i + (U - 1) * G < splits; i += U * G) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const float4*>(p + (int64_t)(i + u * G) * slab);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        acc[u].x += v[u].x; acc[u].y += v[u].y; acc[u].z += v[u].z; acc[u].w += v[u].w;
+      }
+    }
+    for (; i < splits; i += G) {
+      const float4 v = *reinterpret_cast<const float4*>(p + (int64_t)i * slab);
+      acc[0].x += v.x; acc[0].y += v.y; acc[0].z += v.z; acc[0].w += v.w;
+    }
+  }
+  float4 t = acc[0];
+#pragma unroll
+  for (int u = 1; u < U; ++u) { t.x += acc[u].x; t.y += acc[u].y; t.z += acc[u].z; t.w += acc[u].w; }
+  red[grp * L + lane] = t;
+  __syncthreads();
+  if (grp == 0 && ok) {
+#pragma unroll
+    for (int g = 1; g < G; ++g) { const float4 v = red[g * L + lane]; t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w; }
+    const float tv[4] = {t.x, t.y, t.z, t.w};
+    const int co = (int)(e0 / Kpad), k0 = (int)(e0 - (int64_t)co * Kpad);
+    const int K = KH * KW * SC;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + j;
+      if (k >= K) continue;
+      const int tap = k / SC, ci = k - tap * SC;
+      if (ci >= Cin) continue;
+      const int kh = tap / KW, kw = tap - kh * KW;
+      float* d = dw + (((int64_t)co * Cin + ci) * KH + kh) * KW + kw;
+      *d = accumulate ? *d + tv[j] : tv[j];
+    }
+  }
+}
+
+// a slab reduce carried by another launch (the next conv's fused backward)
+struct ReduceJob {
+  const float* ws;
+  float* dw;
+  int Cout, Kpad, SC, Cin, KH, KW, splits, accumulate, G, nblk;
+};
+
+__host__ __device__ inline int reduce_group(int splits) { return splits >= 64 ? 16 : splits >= 16 ? 4 : 1; }
+__host__ __device__ inline int reduce_blocks(int Cout, int Kpad, int G) {
+  const int64_t quads = (int64_t)Cout * Kpad / 4;
+  const int L = 256 / G;
+  return (int)((quads + L - 1) / L);
+}
+
+__device__ __forceinline__ void run_reduce_job(char* smem, int blk, const ReduceJob& j) {
+  float4* red = reinterpret_cast<float4*>(smem);
+  if (j.G == 16) wgrad_reduce_body<16>(red, blk, j.ws, j.dw, j.Cout, j.Kpad, j.SC, j.Cin, j.KH, j.KW, j.splits,
+                                       j.accumulate);
+  else if (j.G == 4) wgrad_reduce_body<4>(red, blk, j.ws, j.dw, j.Cout, j.Kpad, j.SC, j.Cin, j.KH, j.KW, j.splits,
+                                          j.accumulate);
+  else wgrad_reduce_body<1>(red, blk, j.ws, j.dw, j.Cout, j.Kpad, j.SC, j.Cin, j.KH, j.KW, j.splits, j.accumulate);
+}
+
 }  // namespace

@@ -27,6 +27,13 @@ from ._lib import DT_BF16, DT_F32, Pose6dError, call, query, require_device, str
 DTYPES = {torch.float32: DT_F32, torch.bfloat16: DT_BF16}
 
 
+class _WgradReduce(ctypes.Structure):
+    """pose6d_wgrad_reduce_t (include/pose6d.h)."""
+    _fields_ = [("ws", ctypes.c_void_p), ("dw", ctypes.c_void_p)] + [
+        (n, ctypes.c_int32) for n in ("dtype", "N", "H", "W", "Cin", "Cin_real", "Cout", "KH", "KW", "stride", "pad",
+                                      "Ho", "Wo", "accumulate")]
+
+
 _DESC = np.dtype([("w", "<u8"), ("wp", "<u8"), ("wt", "<u8"), ("O", "<i4"), ("I", "<i4"), ("Ip", "<i4"),
                   ("KH", "<i4"), ("KW", "<i4"), ("Kpad", "<i4"), ("start", "<i8"), ("count", "<i8")])
 
@@ -195,6 +202,7 @@ class TrunkEngine:
             elif isinstance(op, _PoolOp):
                 op.argmax = torch.empty(B, o.H, o.W, o.C, device=device, dtype=torch.uint8)
         self.ws_wgrad = f32(max(ws_w // 4, 1))
+        self.ws_wgrad2 = f32(max(ws_w // 4, 1))   # ping-pong: a deferred slab reduce reads the other one
         # BN-backward partials from the data-gradient epilogue (opt-in, POSE6D_BN_EPI=1):
         # the conv whose input is an ActOp's output writes that BN's (sum dz, sum dz *
         # xhat) per 64-pixel tile and the standalone reduce pass is skipped.  Measured
@@ -311,6 +319,17 @@ class TrunkEngine:
         for op in self.ops:
             op.out.pending = None
         self.input.pending = None
+        # weight-gradient slab reduces ride on the next conv's fused launch
+        # (pose6d_conv2d_backward_chain): `pending` = the conv whose dW still waits
+        ws_pp = (self.ws_wgrad, self.ws_wgrad2)
+        slot = 0
+        pending, pending_op = None, None
+        deferred = ctypes.c_int32(0)
+
+        def conv_done(o):
+            if on_conv_done is not None:
+                on_conv_done(o)
+
         for op in reversed(self.ops):
             if isinstance(op, _ActOp):
                 c = op.cop
@@ -354,13 +373,20 @@ class TrunkEngine:
                         src.pending = op.dres
                     else:
                         dx = src.g
+                if op.conv.bias is not None:   # before conv_done(op) can mark the bucket ready
+                    call("channel_sum", dt, dy, M, op.cout, grad_of(op.conv.bias), acc, st)
                 # data + weight gradient: one fused launch on the bf16 fast path
-                args = (dt, op.src.t, dy, op.wt, dres, dx, grad_of(op.conv.weight), acc, self.ws_wgrad,
-                        self.ws_wgrad.numel() * 4, B, op.H, op.W, op.cin_pad, op.cin, op.cout, op.k, op.k,
-                        op.stride, op.pad, op.Ho, op.Wo)
+                ws = ws_pp[slot]
+                dw = grad_of(op.conv.weight)
+                args = (dt, op.src.t, dy, op.wt, dres, dx, dw, acc, ws, ws.numel() * 4, B, op.H, op.W, op.cin_pad,
+                        op.cin, op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo)
                 a = op.bn_act
                 if a is not None and op.bn_rows > 0 and dx is op.src.g:
                     # dx is the final dout of BN `a`: its partial sums come out of this epilogue
+                    if pending is not None:
+                        call("wgrad_reduce", ctypes.addressof(pending), st)
+                        conv_done(pending_op)
+                        pending, pending_op = None, None
                     ac = a.cop
                     plain_a = a.relu and a.res_act is None and a.res_conv is None
                     mk = 2 if plain_a else (1 if a.relu else 0)
@@ -368,16 +394,28 @@ class TrunkEngine:
                          ac.scale if mk == 2 else None, ac.shift if mk == 2 else None, ac.mean, ac.inv,
                          op.bn_part, op.bn_rows, mk, st)
                     a.bn_ready = (op.bn_part, op.bn_rows)
+                    conv_done(op)
                 else:
-                    call("conv2d_backward", *args, st)
-                if op.conv.bias is not None:
-                    call("channel_sum", dt, dy, M, op.cout, grad_of(op.conv.bias), acc, st)
-                if on_conv_done is not None:
-                    on_conv_done(op)
+                    job = _WgradReduce(ws.data_ptr(), dw.data_ptr(), dt, B, op.H, op.W, op.cin_pad, op.cin, op.cout,
+                                       op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, acc)
+                    call("conv2d_backward_chain", *args, ctypes.addressof(pending) if pending is not None else None,
+                         ctypes.addressof(deferred), st)
+                    if pending_op is not None:
+                        conv_done(pending_op)          # its reduce ran in this launch (or just before it)
+                    if deferred.value:
+                        pending, pending_op = job, op
+                        slot ^= 1
+                    else:
+                        pending, pending_op = None, None
+                        conv_done(op)
+
             else:
                 s = op.src
                 call("maxpool_bwd", dt, op.out.g, op.argmax, s.g, B, s.H, s.W, s.C, op.k, op.s, op.p, op.out.H,
                      op.out.W, st)
+        if pending is not None:
+            call("wgrad_reduce", ctypes.addressof(pending), st)
+            conv_done(pending_op)
 
     def _has_later_consumer(self, op):
         """True if op.src is also consumed by a conv processed later in backward

@@ -211,6 +211,26 @@ int pose6d_conv2d_backward_bn(int32_t dtype, const void *x, const void *dy, cons
                               int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, const void *bn_y,
                               const void *bn_out, const float *bn_rs, const float *bn_rb, const float *bn_mean,
                               const float *bn_invstd, float *bn_part, int32_t bn_rows, int32_t bn_mk, void *stream);
+/* Backward chaining across convs: a weight-gradient slab reduce described by
+ * pose6d_wgrad_reduce_t (the conv's geometry as passed to pose6d_conv2d_backward,
+ * its workspace of slabs and its dW) can ride on the NEXT conv's fused launch as
+ * extra workgroups instead of a launch of its own.
+ * pose6d_conv2d_backward_chain = pose6d_conv2d_backward that (a) also reduces
+ * `prev` (NULL = none; its slabs must be in a different workspace) and (b) when
+ * this conv runs the fused kernel, leaves its OWN reduce pending: *deferred = 1,
+ * and the caller passes it as `prev` to the next call or flushes it with
+ * pose6d_wgrad_reduce.  *deferred = 0: this conv's dW is complete. */
+typedef struct {
+  const float *ws;
+  float *dw;
+  int32_t dtype, N, H, W, Cin, Cin_real, Cout, KH, KW, stride, pad, Ho, Wo, accumulate;
+} pose6d_wgrad_reduce_t;
+int pose6d_wgrad_reduce(const pose6d_wgrad_reduce_t *job, void *stream);
+int pose6d_conv2d_backward_chain(int32_t dtype, const void *x, const void *dy, const void *wt, const void *dres,
+                                 void *dx, float *dw, int32_t accumulate, float *workspace, int64_t ws_bytes,
+                                 int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout,
+                                 int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
+                                 const pose6d_wgrad_reduce_t *prev, int32_t *deferred, void *stream);
 /* (1 << 16) | (data-gradient mode << 4) | ring stages when pose6d_conv2d_backward
  * runs ONE fused conv_bwd_kernel<mode, stages, 3> launch (+ the reduce), else 0 */
 int pose6d_bwd_variant(int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH,
