@@ -237,7 +237,8 @@ __global__ __launch_bounds__(kThreads) void bn_act_kernel(const T* __restrict__ 
                                                           const float* __restrict__ shift, const T* __restrict__ res,
                                                           const float* __restrict__ rscale,
                                                           const float* __restrict__ rshift, int relu,
-                                                          T* __restrict__ out, int64_t M, int C) {
+                                                          T* __restrict__ out, int64_t M, int C,
+                                                          uint8_t* __restrict__ mbits) {
   constexpr int E = V<T>::E;
   const int cpr = C / E;
   const int64_t total = M * cpr;
@@ -263,6 +264,13 @@ __global__ __launch_bounds__(kThreads) void bn_act_kernel(const T* __restrict__ 
       for (int e = 0; e < E; ++e) v[e] = fmaxf(v[e], 0.f);
     }
     store_vec(out + off, v);
+    if (mbits) {
+      // bit e = (stored out > 0): the backward's ReLU mask without re-reading `out`
+      unsigned b = 0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) b |= (p6::to_f(p6::from_f<T>(v[e])) > 0.f ? 1u : 0u) << e;
+      mbits[i] = (uint8_t)b;
+    }
   }
 }
 
@@ -287,6 +295,9 @@ __device__ __forceinline__ void relu_mask(float (&d)[V<T>::E], const uint4& ov, 
       const float v = p6::to_f(p6::from_f<T>(fmaf(yy[e], rs[c0 + e], rb[c0 + e])));
       d[e] = v > 0.f ? d[e] : 0.f;
     }
+  } else if constexpr (MK == 3) {   // one mask byte per chunk (bn_act_fwd's bits), in ov.x
+#pragma unroll
+    for (int e = 0; e < E; ++e) d[e] = (ov.x >> e) & 1u ? d[e] : 0.f;
   }
 }
 
@@ -322,6 +333,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce2_kernel(const T* __res
       const int64_t off = (r + u * RL) * C + c0;
       dv[u] = *reinterpret_cast<const uint4*>(dout + off);
       if constexpr (MK == 1) ov[u] = *reinterpret_cast<const uint4*>(out + off);
+      if constexpr (MK == 3) ov[u].x = reinterpret_cast<const uint8_t*>(out)[off / E];
       yv[u] = *reinterpret_cast<const uint4*>(y + off);
     }
 #pragma unroll
@@ -343,6 +355,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce2_kernel(const T* __res
     uint4 ov{};
     load_vec(dout + off, d);
     if constexpr (MK == 1) ov = *reinterpret_cast<const uint4*>(out + off);
+    if constexpr (MK == 3) ov.x = reinterpret_cast<const uint8_t*>(out)[off / E];
     load_vec(y + off, yy);
     relu_mask<MK, T>(d, ov, yy, rs, rb, c0);
 #pragma unroll
@@ -422,6 +435,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const T* __restr
     uint4 ov{};
     load_vec(dout + off, d);
     if constexpr (MK == 1) ov = *reinterpret_cast<const uint4*>(out + off);
+    if constexpr (MK == 3) ov.x = reinterpret_cast<const uint8_t*>(out)[off / E];
     load_vec(y + off, yy);
     relu_mask<MK, T>(d, ov, yy, rs, rb, c0);
     if (dz_out) store_vec(dz_out + off, d);
@@ -501,30 +515,62 @@ extern "C" int pose6d_bn_finalize(const float* partial, int32_t rows, int32_t C,
   return POSE6D_OK;
 }
 
-extern "C" int pose6d_bn_act_fwd(int32_t dtype, const void* y, const float* scale, const float* shift,
-                                 const void* res, const float* res_scale, const float* res_shift, int32_t relu,
-                                 void* out, int64_t M, int32_t C, void* stream) {
+extern "C" int pose6d_bn_act_fwd_mask(int32_t dtype, const void* y, const float* scale, const float* shift,
+                                      const void* res, const float* res_scale, const float* res_shift, int32_t relu,
+                                      void* out, uint8_t* relu_mask, int64_t M, int32_t C, void* stream) {
   P6_CHECK_ARG(C % 8 == 0, "pose6d_bn_act_fwd: C %% 8 != 0");
   hipStream_t s = p6::stream_of(stream);
   if (dtype == POSE6D_DT_BF16)
     bn_act_kernel<bf16><<<grid_for(M * C / 8), kThreads, 0, s>>>((const bf16*)y, scale, shift, (const bf16*)res,
-                                                                   res_scale, res_shift, relu, (bf16*)out, M, C);
+                                                                   res_scale, res_shift, relu, (bf16*)out, M, C,
+                                                                   relu_mask);
   else
     bn_act_kernel<float><<<grid_for(M * C / 4), kThreads, 0, s>>>((const float*)y, scale, shift, (const float*)res,
-                                                                    res_scale, res_shift, relu, (float*)out, M, C);
+                                                                    res_scale, res_shift, relu, (float*)out, M, C,
+                                                                    relu_mask);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
 
+extern "C" int pose6d_bn_act_fwd(int32_t dtype, const void* y, const float* scale, const float* shift,
+                                 const void* res, const float* res_scale, const float* res_shift, int32_t relu,
+                                 void* out, int64_t M, int32_t C, void* stream) {
+  return pose6d_bn_act_fwd_mask(dtype, y, scale, shift, res, res_scale, res_shift, relu, out, nullptr, M, C, stream);
+}
+
 extern "C" int pose6d_bn_bwd_workspace_rows(int64_t M) { return p6::ceil_div(M, rows_per_block(M)); }
+
+namespace {
+int bn_bwd_impl(int mk, int32_t dtype, const void* dout, const void* out, const float* relu_scale,
+                const float* relu_shift, const void* y, const float* mean, const float* invstd, const float* gamma,
+                float* dgamma, float* dbeta, int32_t accumulate, void* dy, void* dz_out, float* workspace, int64_t M,
+                int32_t C, void* stream);
+}  // namespace
 
 extern "C" int pose6d_bn_bwd(int32_t dtype, const void* dout, const void* out, const float* relu_scale,
                              const float* relu_shift, const void* y, const float* mean, const float* invstd,
                              const float* gamma, float* dgamma, float* dbeta, int32_t accumulate, void* dy,
                              void* dz_out, float* workspace, int64_t M, int32_t C, void* stream) {
-  P6_CHECK_ARG(C % 8 == 0 && M > 0, "pose6d_bn_bwd: bad sizes");
   P6_CHECK_ARG(!relu_scale == !relu_shift, "pose6d_bn_bwd: relu_scale and relu_shift go together");
-  const int mk = out ? 1 : relu_scale ? 2 : 0;
+  return bn_bwd_impl(out ? 1 : relu_scale ? 2 : 0, dtype, dout, out, relu_scale, relu_shift, y, mean, invstd, gamma,
+                     dgamma, dbeta, accumulate, dy, dz_out, workspace, M, C, stream);
+}
+
+extern "C" int pose6d_bn_bwd_mask(int32_t dtype, const void* dout, const uint8_t* relu_mask, const void* y,
+                                  const float* mean, const float* invstd, const float* gamma, float* dgamma,
+                                  float* dbeta, int32_t accumulate, void* dy, void* dz_out, float* workspace, int64_t M,
+                                  int32_t C, void* stream) {
+  P6_CHECK_ARG(relu_mask != nullptr, "pose6d_bn_bwd_mask: null mask");
+  return bn_bwd_impl(3, dtype, dout, relu_mask, nullptr, nullptr, y, mean, invstd, gamma, dgamma, dbeta, accumulate,
+                     dy, dz_out, workspace, M, C, stream);
+}
+
+namespace {
+int bn_bwd_impl(int mk, int32_t dtype, const void* dout, const void* out, const float* relu_scale,
+                const float* relu_shift, const void* y, const float* mean, const float* invstd, const float* gamma,
+                float* dgamma, float* dbeta, int32_t accumulate, void* dy, void* dz_out, float* workspace, int64_t M,
+                int32_t C, void* stream) {
+  P6_CHECK_ARG(C % 8 == 0 && M > 0, "pose6d_bn_bwd: bad sizes");
   hipStream_t s = p6::stream_of(stream);
   const int rpb = rows_per_block(M);
   const int nb = p6::ceil_div(M, rpb);
@@ -538,7 +584,7 @@ extern "C" int pose6d_bn_bwd(int32_t dtype, const void* dout, const void* out, c
   auto reduce = [&](auto* typed) {
     using TT = std::remove_pointer_t<decltype(typed)>;
     auto k = mk == 1 ? bn_bwd_reduce2_kernel<TT, 1> : mk == 2 ? bn_bwd_reduce2_kernel<TT, 2>
-                                                              : bn_bwd_reduce2_kernel<TT, 0>;
+           : mk == 3 ? bn_bwd_reduce2_kernel<TT, 3> : bn_bwd_reduce2_kernel<TT, 0>;
     k<<<grid, kThreads, 0, s>>>((const TT*)dout, (const TT*)out, relu_scale, relu_shift, (const TT*)y, mean, invstd,
                                 part, M, C, rpb);
   };
@@ -550,7 +596,8 @@ extern "C" int pose6d_bn_bwd(int32_t dtype, const void* dout, const void* out, c
   P6_LAUNCH_CHECK();
   auto apply = [&](auto* typed) {
     using TT = std::remove_pointer_t<decltype(typed)>;
-    auto k = mk == 1 ? bn_bwd_apply_kernel<TT, 1> : mk == 2 ? bn_bwd_apply_kernel<TT, 2> : bn_bwd_apply_kernel<TT, 0>;
+    auto k = mk == 1 ? bn_bwd_apply_kernel<TT, 1> : mk == 2 ? bn_bwd_apply_kernel<TT, 2>
+           : mk == 3 ? bn_bwd_apply_kernel<TT, 3> : bn_bwd_apply_kernel<TT, 0>;
     k<<<grid_for(M * C / V<TT>::E), kThreads, 0, s>>>((const TT*)dout, (const TT*)out, relu_scale, relu_shift,
                                                       (const TT*)y, mean, invstd, coef, (TT*)dy, (TT*)dz_out, M, C);
   };
@@ -559,6 +606,7 @@ extern "C" int pose6d_bn_bwd(int32_t dtype, const void* dout, const void* out, c
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
+}  // namespace
 
 extern "C" int pose6d_channel_sum(int32_t dtype, const void* x, int64_t M, int32_t C, float* out, int32_t accumulate,
                                   void* stream) {
@@ -589,7 +637,8 @@ extern "C" int pose6d_bn_bwd_finish(int32_t dtype, const void* dout, const void*
   P6_LAUNCH_CHECK();
   auto apply = [&](auto* typed) {
     using TT = std::remove_pointer_t<decltype(typed)>;
-    auto k = mk == 1 ? bn_bwd_apply_kernel<TT, 1> : mk == 2 ? bn_bwd_apply_kernel<TT, 2> : bn_bwd_apply_kernel<TT, 0>;
+    auto k = mk == 1 ? bn_bwd_apply_kernel<TT, 1> : mk == 2 ? bn_bwd_apply_kernel<TT, 2>
+           : mk == 3 ? bn_bwd_apply_kernel<TT, 3> : bn_bwd_apply_kernel<TT, 0>;
     k<<<grid_for(M * C / V<TT>::E), kThreads, 0, s>>>((const TT*)dout, (const TT*)out, relu_scale, relu_shift,
                                                       (const TT*)y, mean, invstd, coef, (TT*)dy, (TT*)dz_out, M, C);
   };

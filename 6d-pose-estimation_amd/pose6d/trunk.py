@@ -199,6 +199,10 @@ class TrunkEngine:
                 op.dres = e(B, op.H, op.W, op.cin_pad) if op.needs_dgrad else None
             elif isinstance(op, _ActOp):
                 op.dz = e(B, o.H, o.W, o.C) if (op.res_act is not None or op.res_conv is not None) else None
+                # residual BN + ReLU: one mask bit per element replaces re-reading `out` in backward
+                vec = 8 if dtype == torch.bfloat16 else 4
+                op.mbits = (torch.empty(B * o.H * o.W * o.C // vec, device=device, dtype=torch.uint8)
+                            if (op.relu and op.dz is not None) else None)
             elif isinstance(op, _PoolOp):
                 op.argmax = torch.empty(B, o.H, o.W, o.C, device=device, dtype=torch.uint8)
         self.ws_wgrad = f32(max(ws_w // 4, 1))
@@ -286,13 +290,14 @@ class TrunkEngine:
             elif isinstance(op, _ActOp):
                 c = op.cop
                 M = B * c.Ho * c.Wo
+                mb = op.mbits if training else None
                 if op.res_conv is not None:
                     r = op.res_conv
-                    call("bn_act_fwd", dt, c.out.t, c.scale, c.shift, r.out.t, r.scale, r.shift, int(op.relu),
-                         op.out.t, M, c.cout, st)
+                    call("bn_act_fwd_mask", dt, c.out.t, c.scale, c.shift, r.out.t, r.scale, r.shift, int(op.relu),
+                         op.out.t, mb, M, c.cout, st)
                 else:
-                    call("bn_act_fwd", dt, c.out.t, c.scale, c.shift, op.res_act.t if op.res_act else None, None,
-                         None, int(op.relu), op.out.t, M, c.cout, st)
+                    call("bn_act_fwd_mask", dt, c.out.t, c.scale, c.shift, op.res_act.t if op.res_act else None, None,
+                         None, int(op.relu), op.out.t, mb, M, c.cout, st)
             else:
                 s = op.src
                 call("maxpool_fwd", dt, s.t, op.out.t, op.argmax, B, s.H, s.W, s.C, op.k, op.s, op.p, op.out.H,
@@ -347,6 +352,9 @@ class TrunkEngine:
                     call("bn_bwd_finish", dt, op.out.g, out, rs, rb, c.out.t, c.mean, c.inv, bn.weight.detach(),
                          grad_of(bn.weight), grad_of(bn.bias), acc, c.out.g, op.dz, part, rows, self.ws_bn, M,
                          c.cout, st)
+                elif op.mbits is not None:
+                    call("bn_bwd_mask", dt, op.out.g, op.mbits, c.out.t, c.mean, c.inv, bn.weight.detach(),
+                         grad_of(bn.weight), grad_of(bn.bias), acc, c.out.g, op.dz, self.ws_bn, M, c.cout, st)
                 else:
                     call("bn_bwd", dt, op.out.g, out, rs, rb, c.out.t, c.mean, c.inv, bn.weight.detach(),
                          grad_of(bn.weight), grad_of(bn.bias), acc, c.out.g, op.dz, self.ws_bn, M, c.cout, st)

@@ -251,6 +251,11 @@ int pose6d_bn_finalize(const float *partial, int32_t rows, int32_t C, int64_t co
 int pose6d_bn_act_fwd(int32_t dtype, const void *y, const float *scale, const float *shift, const void *res,
                       const float *res_scale, const float *res_shift, int32_t relu, void *out, int64_t M, int32_t C,
                       void *stream);
+/* bn_act_fwd that also writes relu_mask[M * C / E] (E = 8 bf16 / 4 fp32 elements per
+ * byte, bit e of byte i = out[i * E + e] > 0) for pose6d_bn_bwd_mask. */
+int pose6d_bn_act_fwd_mask(int32_t dtype, const void *y, const float *scale, const float *shift, const void *res,
+                           const float *res_scale, const float *res_shift, int32_t relu, void *out, uint8_t *relu_mask,
+                           int64_t M, int32_t C, void *stream);
 /* backward of bn_act_fwd for one BN: dz = dout * mask, mask = out > 0 when `out` is
  * given, else (relu_scale/relu_shift given: a ReLU BN without residual) the sign
  * bn_act_fwd stored, recomputed from y as round(y * relu_scale + relu_shift) > 0
@@ -258,6 +263,11 @@ int pose6d_bn_act_fwd(int32_t dtype, const void *y, const float *scale, const fl
  * overwrite); dy; dz_out (if non-NULL) = dz.
  * workspace: (pose6d_bn_bwd_workspace_rows(M) * 2 + 3) * C floats. */
 int pose6d_bn_bwd_workspace_rows(int64_t M);
+/* pose6d_bn_bwd with the ReLU mask taken from pose6d_bn_act_fwd_mask's bits instead of
+ * re-reading the forward output (the residual BNs: 1/16 of the bytes). */
+int pose6d_bn_bwd_mask(int32_t dtype, const void *dout, const uint8_t *relu_mask, const void *y, const float *mean,
+                       const float *invstd, const float *gamma, float *dgamma, float *dbeta, int32_t accumulate,
+                       void *dy, void *dz_out, float *workspace, int64_t M, int32_t C, void *stream);
 int pose6d_bn_bwd(int32_t dtype, const void *dout, const void *out, const float *relu_scale,
                   const float *relu_shift, const void *y, const float *mean, const float *invstd, const float *gamma,
                   float *dgamma, float *dbeta, int32_t accumulate, void *dy, void *dz_out, float *workspace,
