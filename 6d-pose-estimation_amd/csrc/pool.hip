@@ -51,11 +51,26 @@ struct PackDesc {
   int64_t start, count;
 };
 
-// z = 0: wp[o][k], k = (kh, kw, ci): each OIHW row o is staged in LDS (coalesced
-//        row read), then written in (kh, kw, ci) order with channel / K padding.
+// z = 0: wp[o][k], k = (kh, kw, ci).  1x1 filters (k order == OIHW order): a straight
+//        fp32 -> compute-dtype conversion, 8 elements per thread (two float4 loads, one
+//        16-B store).  Larger filters: each OIHW row o is staged in LDS with float4
+//        loads, then written in (kh, kw, ci) order two elements per store, with
+//        channel / K padding.
 // z = 1: wt[(ci, kh, kw)][o] is the transpose of w viewed as [O][I*KH*KW]: 64 x 64
-//        tiles through LDS, coalesced on both sides.
+//        tiles through LDS, float4 loads, two-element stores.
 constexpr int kPackRow = 4608;   // largest staged row (512 x 3 x 3); longer rows gather directly
+
+template <typename T>
+__device__ __forceinline__ void store2(T* p, float a, float b) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16 v[2] = {(bf16)a, (bf16)b};
+    uint32_t u;
+    __builtin_memcpy(&u, v, 4);
+    *reinterpret_cast<uint32_t*>(p) = u;
+  } else {
+    *reinterpret_cast<float2*>(p) = make_float2(a, b);
+  }
+}
 
 template <typename T>
 __global__ __launch_bounds__(kThreads) void pack_kernel(const PackDesc* __restrict__ descs) {
@@ -63,42 +78,88 @@ __global__ __launch_bounds__(kThreads) void pack_kernel(const PackDesc* __restri
   const PackDesc d = descs[blockIdx.y];
   const int taps = d.KH * d.KW;
   const int R = d.I * taps;
+  const int tid = threadIdx.x;
   if (blockIdx.z == 0) {
     const int K = taps * d.Ip;
+    if (taps == 1 && d.Ip == d.I && d.Kpad == d.I && (d.I & 7) == 0) {
+      const int64_t n8 = (int64_t)d.O * d.I / 8;
+      for (int64_t q = blockIdx.x * (int64_t)kThreads + tid; q < n8; q += (int64_t)gridDim.x * kThreads) {
+        const float4 a = *reinterpret_cast<const float4*>(d.w + q * 8);
+        const float4 b = *reinterpret_cast<const float4*>(d.w + q * 8 + 4);
+        T* dst = reinterpret_cast<T*>(d.wp) + q * 8;
+        store2(dst, a.x, a.y);
+        store2(dst + 2, a.z, a.w);
+        store2(dst + 4, b.x, b.y);
+        store2(dst + 6, b.z, b.w);
+      }
+      return;
+    }
+    const bool vec = (R & 3) == 0 && R <= kPackRow;
     for (int o = blockIdx.x; o < d.O; o += gridDim.x) {
       const float* row = d.w + (int64_t)o * R;
       const bool staged = R <= kPackRow;
-      if (staged) {
-        for (int r = threadIdx.x; r < R; r += kThreads) sm[r] = row[r];
+      if (vec) {
+        for (int r = tid * 4; r < R; r += kThreads * 4)
+          *reinterpret_cast<float4*>(sm + r) = *reinterpret_cast<const float4*>(row + r);
+        __syncthreads();
+      } else if (staged) {
+        for (int r = tid; r < R; r += kThreads) sm[r] = row[r];
         __syncthreads();
       }
       T* dst = reinterpret_cast<T*>(d.wp) + (int64_t)o * d.Kpad;
-      for (int k = threadIdx.x; k < d.Kpad; k += kThreads) {
-        float v = 0.f;
-        if (k < K) {
-          const int tap = k / d.Ip, c = k - tap * d.Ip;
-          if (c < d.I) v = staged ? sm[c * taps + tap] : row[c * taps + tap];
+      for (int k = tid * 2; k < d.Kpad; k += kThreads * 2) {   // Kpad is even
+        float v[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int kk = k + h;
+          v[h] = 0.f;
+          if (kk < K) {
+            const int tap = kk / d.Ip, c = kk - tap * d.Ip;
+            if (c < d.I) v[h] = staged ? sm[c * taps + tap] : row[c * taps + tap];
+          }
         }
-        dst[k] = p6::from_f<T>(v);
+        store2(dst + k, v[0], v[1]);
       }
       __syncthreads();
     }
   } else if (d.wt) {
     const int tr = p6::ceil_div(R, 64), to = p6::ceil_div(d.O, 64);
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const bool vec = (R & 3) == 0 && (d.O & 1) == 0;
+    const int tx4 = tid & 15, ty = tid >> 4;        // loads: 16 float4 columns x 16 rows per pass
+    const int px = tid & 31, py = tid >> 5;         // stores: 32 element pairs x 8 rows per pass
     for (int t = blockIdx.x; t < tr * to; t += gridDim.x) {
       const int o0 = (t / tr) * 64, r0 = (t - (t / tr) * tr) * 64;
-#pragma unroll 4
-      for (int i = ty; i < 64; i += 4) {   // rows o0 + i of w, columns r0 + tx
-        const int o = o0 + i, r = r0 + tx;
-        sm[i * 65 + tx] = (o < d.O && r < R) ? d.w[(int64_t)o * R + r] : 0.f;
+#pragma unroll
+      for (int i = ty; i < 64; i += 16) {   // rows o0 + i of w, columns r0 + 4 tx4 ..
+        const int o = o0 + i, r = r0 + 4 * tx4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (o < d.O) {
+          if (vec && r + 3 < R) {
+            v = *reinterpret_cast<const float4*>(d.w + (int64_t)o * R + r);
+          } else {
+            const float* src = d.w + (int64_t)o * R;
+            v.x = r < R ? src[r] : 0.f;
+            v.y = r + 1 < R ? src[r + 1] : 0.f;
+            v.z = r + 2 < R ? src[r + 2] : 0.f;
+            v.w = r + 3 < R ? src[r + 3] : 0.f;
+          }
+        }
+        float* q = sm + i * 65 + 4 * tx4;
+        q[0] = v.x; q[1] = v.y; q[2] = v.z; q[3] = v.w;
       }
       __syncthreads();
       T* wt = reinterpret_cast<T*>(d.wt);
-#pragma unroll 4
-      for (int i = ty; i < 64; i += 4) {   // rows r0 + i of wt, columns o0 + tx
-        const int r = r0 + i, o = o0 + tx;
-        if (r < R && o < d.O) wt[(int64_t)r * d.O + o] = p6::from_f<T>(sm[tx * 65 + i]);
+#pragma unroll
+      for (int i = py; i < 64; i += 8) {   // rows r0 + i of wt, columns o0 + 2 px ..
+        const int r = r0 + i, o = o0 + 2 * px;
+        if (r >= R) continue;
+        const float a = sm[(2 * px) * 65 + i], b = sm[(2 * px + 1) * 65 + i];
+        if (vec && o + 1 < d.O) {
+          store2(wt + (int64_t)r * d.O + o, a, b);
+        } else {
+          if (o < d.O) wt[(int64_t)r * d.O + o] = p6::from_f<T>(a);
+          if (o + 1 < d.O) wt[(int64_t)r * d.O + o + 1] = p6::from_f<T>(b);
+        }
       }
       __syncthreads();
     }
@@ -270,7 +331,7 @@ extern "C" int pose6d_pack_conv_weights(int32_t dtype, const void* descs, int32_
   if (n_desc == 0) return POSE6D_OK;
   P6_CHECK_ARG(n_desc <= 65535, "pose6d_pack_conv_weights: too many descriptors");
   hipStream_t s = p6::stream_of(stream);
-  dim3 grid(128, n_desc, 2);
+  dim3 grid(256, n_desc, 2);
   if (dtype == POSE6D_DT_BF16) pack_kernel<bf16><<<grid, kThreads, 0, s>>>((const PackDesc*)descs);
   else pack_kernel<float><<<grid, kThreads, 0, s>>>((const PackDesc*)descs);
   P6_LAUNCH_CHECK();

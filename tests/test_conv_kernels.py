@@ -301,3 +301,26 @@ def test_pools(dtype):
     f = torch.empty(2, 64, device=dev)
     call("avgpool_fwd", 0, _nhwc(x).to(dev), f, 2, 49, 64, stream())
     _close(f, x.mean((2, 3)), 1e-6, "avgpool")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("O,I,k,cpad", [(64, 3, 7, 4), (256, 64, 1, 64), (64, 64, 3, 64), (512, 512, 3, 512),
+                                         (2048, 1024, 1, 1024), (100, 72, 3, 72)])
+def test_pack_layouts(dtype, O, I, k, cpad):
+    """pose6d_pack_conv_weights: wp[o][(kh, kw, ci)] with channel / K zero padding and
+    wt[ci][kh][kw][o], exactly the dtype-rounded OIHW values."""
+    from pose6d.trunk import pack_single
+    g = torch.Generator(device="cuda").manual_seed(O + I + k)
+    w = torch.randn(O, I, k, k, device="cuda", generator=g)
+    wp, wt = pack_single(w, cpad, dtype, with_t=I >= 8)
+    torch.cuda.synchronize()
+    ref = torch.zeros(O, k, k, cpad, device="cuda")
+    ref[..., :I] = w.permute(0, 2, 3, 1)
+    ref = ref.reshape(O, -1)
+    Kpad = wp.shape[1]
+    full = torch.zeros(O, Kpad, device="cuda")
+    full[:, :ref.shape[1]] = ref
+    assert torch.equal(wp.float(), full.to(dtype).float())
+    if I >= 8:
+        assert torch.equal(wt.float(), w.permute(1, 2, 3, 0).to(dtype).float())
