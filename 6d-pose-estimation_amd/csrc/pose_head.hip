@@ -193,6 +193,68 @@ __global__ void pose_loss_bwd_kernel(const float* __restrict__ pr, const float* 
   }
 }
 
+// The whole quaternion / translation head + PoseLoss forward and backward of the
+// RGBD-Geometric training step in ONE single-block launch (it was five launches of
+// a few threads each): per sample, exactly the arithmetic of rownorm_fwd,
+// pinhole_depth, pose_loss_fwd / _bwd (dloss = 1) and rownorm_bwd above, and the
+// loss reduced in pose_loss_fwd's order (rot / trans / loss bit-identical; the
+// normalize backward may differ by fp contraction).
+__global__ __launch_bounds__(kThreads) void geo_head_loss_kernel(
+    const float* __restrict__ raw, const float* __restrict__ depth, int H, int W, const float* __restrict__ bbox,
+    const float* __restrict__ K, int Kb, const float* __restrict__ gr, const float* __restrict__ gt, int64_t B,
+    float wr, float wt, int mode, float* __restrict__ rot, float* __restrict__ trans, float* __restrict__ loss,
+    float* __restrict__ draw, float* __restrict__ dtrans) {
+  __shared__ float red[2][kThreads / 64];
+  float sr = 0.f, st = 0.f;
+  const float grot_scale = wr / (float)B, c = wt / (float)(3 * B);
+  for (int64_t b = threadIdx.x; b < B; b += kThreads) {
+    // F.normalize(raw) -> rot (pose_net_rgbd_geometric.py:45)
+    const float* xr = raw + 4 * b;
+    const float n = l2(xr, 4);
+    const float d = fmaxf(n, kNormEps);
+    float q[4];
+    for (int i = 0; i < 4; ++i) { q[i] = xr[i] / d; rot[4 * b + i] = q[i]; }
+    // pinhole translation (pose_net_rgbd_geometric.py:56-85)
+    float fx, fy, cx, cy;
+    load_K(K, Kb, b, fx, fy, cx, cy);
+    const float u = fminf(fmaxf(bbox[2 * b], 0.f), 223.f);
+    const float v = fminf(fmaxf(bbox[2 * b + 1], 0.f), 223.f);
+    const int ui = min(max((int)u, 0), 223);
+    const int vi = min(max((int)v, 0), 223);
+    float z = depth[(int64_t)b * H * W + (int64_t)vi * W + ui];
+    z = z > 0.01f ? z : 0.5f;
+    z = fminf(fmaxf(z, 0.1f), 2.0f);
+    const float t[3] = {(u - cx) * z / fx, (v - cy) * z / fy, z};
+    // PoseLoss forward + backward w.r.t. rot / trans
+    float drot[4];
+    sr += rot_term(q, gr + 4 * b, mode, drot, grot_scale);
+    for (int i = 0; i < 3; ++i) {
+      trans[3 * b + i] = t[i];
+      st += fabsf(t[i] - gt[3 * b + i]);
+      const float e = t[i] - gt[3 * b + i];
+      dtrans[3 * b + i] = e > 0.f ? c : (e < 0.f ? -c : 0.f);
+    }
+    // back through F.normalize (rownorm_bwd mode 0)
+    if (n > kNormEps) {
+      float xg = 0.f;
+      for (int i = 0; i < 4; ++i) xg = fmaf(xr[i], drot[i], xg);
+      const float inv = 1.0f / n, cc = xg * inv * inv * inv;
+      for (int i = 0; i < 4; ++i) draw[4 * b + i] = drot[i] * inv - xr[i] * cc;
+    } else {
+      for (int i = 0; i < 4; ++i) draw[4 * b + i] = drot[i] / kNormEps;
+    }
+  }
+  sr = p6::wave_sum(sr);
+  st = p6::wave_sum(st);
+  if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = sr; red[1][threadIdx.x >> 6] = st; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.f, cc = 0.f;
+    for (int i = 0; i < kThreads / 64; ++i) { a += red[0][i]; cc += red[1][i]; }
+    loss[0] = wr * (a / (float)B) + wt * (cc / (float)(3 * B));
+  }
+}
+
 inline unsigned nblk(int64_t n) { return (unsigned)((n + kThreads - 1) / kThreads); }
 
 }  // namespace
@@ -260,6 +322,20 @@ extern "C" int pose6d_pose_loss_bwd(const float* pred_rot, const float* pred_tra
   pose_loss_bwd_kernel<<<nblk(B), kThreads, 0, p6::stream_of(stream)>>>(pred_rot, pred_trans, gt_rot, gt_trans, B,
                                                                         rot_weight, trans_weight, rot_mode, dloss,
                                                                         grad_rot, grad_trans);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+extern "C" int pose6d_geo_head_loss(const float* raw, const float* depth_raw, int32_t H, int32_t W,
+                                    const float* bbox_center, const float* K, int32_t K_batched, const float* gt_rot,
+                                    const float* gt_trans, int64_t B, float rot_weight, float trans_weight,
+                                    int32_t rot_mode, float* rot, float* trans, float* loss, float* grad_raw,
+                                    float* grad_trans, void* stream) {
+  P6_CHECK_ARG(H >= 224 && W >= 224, "pose6d_geo_head_loss: the reference clamps to 223, needs H,W >= 224");
+  P6_CHECK_ARG(B > 0 && (rot_mode == 0 || rot_mode == 1), "pose6d_geo_head_loss: bad B / rot_mode");
+  geo_head_loss_kernel<<<1, kThreads, 0, p6::stream_of(stream)>>>(raw, depth_raw, H, W, bbox_center, K, K_batched,
+                                                                  gt_rot, gt_trans, B, rot_weight, trans_weight,
+                                                                  rot_mode, rot, trans, loss, grad_raw, grad_trans);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }

@@ -118,13 +118,11 @@ class RGBDGeometricTrainer:
         st = stream()
         feat = self.trunk.forward(rgb, True, pack=False)
         raw = self.head.forward(feat, True, seed_dev=self.seed, salt=1)
-        call("rownorm_fwd", raw, self.rot, self.B, 4, 0, st)
-        call("pinhole_depth", depth_raw, depth_raw.shape[1], depth_raw.shape[2], bbox, K, 1 if K.dim() == 3 else 0,
-             self.B, self.trans, st)
-        call("pose_loss_fwd", self.rot, self.trans, gt_rot, gt_trans, self.B, self.wr, self.wt, 0, self.loss, st)
-        call("pose_loss_bwd", self.rot, self.trans, gt_rot, gt_trans, self.B, self.wr, self.wt, 0, self.one,
-             self.drot, self.dtrans, st)
-        call("rownorm_bwd", raw, self.drot, self.draw, self.B, 4, 0, st)
+        # F.normalize + pinhole + PoseLoss fwd/bwd + normalize bwd: one launch (the same
+        # arithmetic as the rownorm_* / pinhole_depth / pose_loss_* entry points)
+        call("geo_head_loss", raw, depth_raw, depth_raw.shape[1], depth_raw.shape[2], bbox, K,
+             1 if K.dim() == 3 else 0, gt_rot, gt_trans, self.B, self.wr, self.wt, 0, self.rot, self.trans, self.loss,
+             self.draw, self.dtrans, st)
         return raw
 
     def _head_backward(self):

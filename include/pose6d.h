@@ -108,6 +108,16 @@ int pose6d_pose_loss_bwd(const float *pred_rot, const float *pred_trans, const f
                          int32_t rot_mode, const float *dloss, float *grad_rot, float *grad_trans,
                          void *stream);
 
+/* The RGBD-Geometric training step's head + loss in one launch: rot =
+ * F.normalize(raw) (pose_net_rgbd_geometric.py:45), trans = pinhole(depth_raw)
+ * (:56-85), loss = PoseLoss(rot, trans) (pose_loss.py:19-28) and its gradient for
+ * dloss = 1: grad_raw (through the normalize) and grad_trans.  Same formulas as the
+ * separate pose6d_rownorm_* / pinhole_depth / pose_loss_* calls. */
+int pose6d_geo_head_loss(const float *raw, const float *depth_raw, int32_t H, int32_t W, const float *bbox_center,
+                         const float *K, int32_t K_batched, const float *gt_rot, const float *gt_trans, int64_t B,
+                         float rot_weight, float trans_weight, int32_t rot_mode, float *rot, float *trans,
+                         float *loss, float *grad_raw, float *grad_trans, void *stream);
+
 /* ------------------------------------------------------------------------
  * Input crops -- replaces the per-sample body of LineMODDatasetRGBD.__getitem__
  * after the file reads (data/dataset_rgbd.py:104-206; dataset_rgb.py:95-145 for

@@ -90,3 +90,29 @@ def test_bn1d_relu_fwd_bwd(M, C):
     # batches, so the absolute tolerance is scaled by gamma * invstd * |dy|, not by |dx|
     scale = ((gamma * si).max() * dy.abs().max()).item()
     torch.testing.assert_close(dx.double(), xr.grad, rtol=1e-4, atol=1e-5 * scale)
+
+
+def test_geo_head_loss_matches_separate_calls():
+    """pose6d_geo_head_loss == rownorm_fwd + pinhole_depth + pose_loss_fwd/_bwd + rownorm_bwd (same formulas;
+    the compiler may contract the normalize-backward differently: 1e-6)."""
+    from pose6d._lib import call, stream
+    from bench import synth_batch
+    B = 32
+    _, depth_raw, bbox, K, gr, gt = synth_batch(B, "cuda", seed=9)
+    raw = torch.randn(B, 4, device="cuda") * 3
+    raw[3] = 0.0                               # zero-norm row (F.normalize eps branch)
+    f = lambda *s: torch.empty(*s, device="cuda")
+    rot, trans, loss, draw, dtr = f(B, 4), f(B, 3), f(()), f(B, 4), f(B, 3)
+    call("geo_head_loss", raw, depth_raw, 224, 224, bbox, K, 1, gr, gt, B, 1.0, 10.0, 0, rot, trans, loss, draw, dtr,
+         stream())
+    rot2, trans2, loss2, drot2, draw2, dtr2 = f(B, 4), f(B, 3), f(()), f(B, 4), f(B, 4), f(B, 3)
+    one = torch.ones((), device="cuda")
+    call("rownorm_fwd", raw, rot2, B, 4, 0, stream())
+    call("pinhole_depth", depth_raw, 224, 224, bbox, K, 1, B, trans2, stream())
+    call("pose_loss_fwd", rot2, trans2, gr, gt, B, 1.0, 10.0, 0, loss2, stream())
+    call("pose_loss_bwd", rot2, trans2, gr, gt, B, 1.0, 10.0, 0, one, drot2, dtr2, stream())
+    call("rownorm_bwd", raw, drot2, draw2, B, 4, 0, stream())
+    torch.cuda.synchronize()
+    for a, b in ((rot, rot2), (trans, trans2), (loss, loss2), (dtr, dtr2)):
+        assert torch.equal(a, b)
+    torch.testing.assert_close(draw, draw2, rtol=1e-6, atol=1e-9)
