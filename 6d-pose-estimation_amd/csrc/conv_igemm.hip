@@ -44,7 +44,23 @@ struct Geom {
   int KH, KW, stride, pad;
   int gm, gn;              // grid in tiles
   int nmajor;              // fast path: tile order N-major (weights larger than the gathered source)
+  int s2one;               // kDgradS2: 0 = grid covers the four parity classes; c + 1 = only class c
 };
+
+// kDgradS2 launched in place (dres == dx) when a single parity class has taps
+// (1x1 stride 2): the other classes' pixels are already final, so the grid covers
+// that class alone instead of launching three workgroups per tile that only exit.
+void s2_single_class(Geom& g, const void* res, const void* out) {
+  g.s2one = 0;
+  if (res != out) return;
+  int n = 0, last = 0;
+  for (int cls = 0; cls < 4; ++cls) {
+    const int kh0 = ((cls >> 1) + g.pad) & 1, kw0 = ((cls & 1) + g.pad) & 1;
+    if (((g.KH - kh0 + 1) >> 1) * ((g.KW - kw0 + 1) >> 1) > 0) { ++n; last = cls; }
+  }
+  if (n == 1) g.s2one = last + 1;
+}
+__host__ __device__ inline int s2_classes(const Geom& g) { return g.s2one ? 1 : 4; }
 
 // BatchNorm backward partials produced by a data-gradient epilogue (bf16 fast path):
 // the dX tile IS the dout of the BN that produced this conv's input, so the
@@ -528,7 +544,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
   static_assert(S >= 2, "ring needs two stages");
 
   const int per = g.gm * g.gn;
-  const int nwg = MODE == kDgradS2 ? 4 * per : per;
+  const int nwg = MODE == kDgradS2 ? s2_classes(g) * per : per;
   int bid = bid_in;
   {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
@@ -539,13 +555,20 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
   // four blocks that gather the same dY rows run on the same L2
   int cls = -1, py = 0, px = 0, kh0 = 0, kw0 = 0, ntx = 1, nk = g.Kpad >> 6;
   if (MODE == kDgradS2) {
-    cls = 3 - (bid & 3);
-    bid >>= 2;
+    if (g.s2one) {
+      cls = g.s2one - 1;
+    } else {
+      cls = 3 - (bid & 3);
+      bid >>= 2;
+    }
     py = cls >> 1; px = cls & 1;
     kh0 = (py + g.pad) & 1; kw0 = (px + g.pad) & 1;   // first tap of this parity, then every 2nd
     const int nty = (g.KH - kh0 + 1) >> 1;
     ntx = (g.KW - kw0 + 1) >> 1;
     nk = (nty * ntx) << (g.log2SC - 6);
+    // a class no tap reaches (1x1 stride 2: three of four) contributes zeros: with
+    // the residual accumulated in place (res == out) its pixels are already final
+    if (nk == 0 && res == out) return;
   }
   // consecutive logical tiles share an XCD (remap above): M-major keeps a few A row
   // blocks + all of B in that XCD's L2, N-major all of A + a slice of B
@@ -796,7 +819,8 @@ int launch_fast(const Geom& g0, const void* src, const void* w, const float* bia
   const int ring = (nk < S ? (nk > 0 ? nk : 1) : S) * (BM + BN) * 128;
   const int epi = BM * (BN * 2 + 16);
   const int lds = ring > epi ? ring : epi;
-  const int grid = g.gm * g.gn * (MODE == kDgradS2 ? 4 : 1);
+  if (MODE == kDgradS2) s2_single_class(g, res, out);
+  const int grid = g.gm * g.gn * (MODE == kDgradS2 ? s2_classes(g) : 1);
   conv_lds_kernel<BM, BN, MODE, S><<<grid, kThreads, lds, s>>>((const bf16*)src, (const bf16*)w, bias,
                                                                 (const bf16*)res, (bf16*)out, stats, g);
   P6_LAUNCH_CHECK();
@@ -1042,7 +1066,8 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
   Geom gd = gd0;
   gd.gm = p6::ceil_div(gd.M, 64);
   gd.gn = p6::ceil_div(gd.Ncols, 64);
-  const int nd = gd.gm * gd.gn * (DMODE == kDgradS2 ? 4 : 1);
+  if (DMODE == kDgradS2 && !bn.part) s2_single_class(gd, dres, dx);
+  const int nd = gd.gm * gd.gn * (DMODE == kDgradS2 ? s2_classes(gd) : 1);
   const int nd_pad = (nd + 7) & ~7;
   const int nw = gw.gm * gw.gn * gw.splits;
   const int nk = fast_nk(DMODE, gd);

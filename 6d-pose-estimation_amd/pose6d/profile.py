@@ -60,7 +60,7 @@ def conv_launches(eng, fused=True):
                              op.pad, op.Ho, op.Wo), T)
 
             def dgrad(op=op):
-                call("conv2d_dgrad", dt, op.out.g, op.wt, None, op.dres, B, op.H, op.W, op.cin_pad, op.cout, op.k,
+                call("conv2d_dgrad", dt, op.out.g, op.wt, None, op.src.g, B, op.H, op.W, op.cin_pad, op.cout, op.k,
                      op.k, op.stride, op.pad, op.Ho, op.Wo, st)
             out.append((sym, flops, dgrad, op.name + ".dgrad"))
         v = query("wgrad_variant", dt, M, op.cout, op.k * op.k * op.cin_pad, op.cin_pad)

@@ -135,13 +135,19 @@ class TrunkEngine:
             for li in range(4):
                 for bi, blk in enumerate(s[4 + li]):
                     nm = f"layer{li + 1}.{bi}"
+                    # the downsample conv runs first in forward, so in backward it comes
+                    # after conv1 and adds its data gradient into conv1's in place: a
+                    # stride-2 1x1 then touches only the even pixels it reaches
+                    # (pose6d_conv2d_backward with dres == dx skips the empty classes)
+                    cd = None
+                    if blk.downsample is not None:
+                        cd = conv_bn(blk.downsample[0], blk.downsample[1], cur, nm + ".down")
                     c1 = conv_bn(blk.conv1, blk.bn1, cur, nm + ".conv1")
                     a1 = _ActOp(c1, True, name=nm + ".a1"); self.ops.append(a1)
                     c2 = conv_bn(blk.conv2, blk.bn2, a1.out, nm + ".conv2")
                     a2 = _ActOp(c2, True, name=nm + ".a2"); self.ops.append(a2)
                     c3 = conv_bn(blk.conv3, blk.bn3, a2.out, nm + ".conv3")
-                    if blk.downsample is not None:
-                        cd = conv_bn(blk.downsample[0], blk.downsample[1], cur, nm + ".down")
+                    if cd is not None:
                         o = _ActOp(c3, True, res_conv=cd, name=nm + ".out")
                     else:
                         o = _ActOp(c3, True, res_act=cur, name=nm + ".out")
@@ -196,7 +202,6 @@ class TrunkEngine:
                 ws_w = max(ws_w, query("conv2d_wgrad_workspace", self.dt, B, op.Ho, op.Wo, op.cin_pad, op.cout, op.k,
                                        op.k))
                 ws_bn = max(ws_bn, (query("bn_bwd_workspace_rows", M) * 2 + 3) * op.cout)
-                op.dres = e(B, op.H, op.W, op.cin_pad) if op.needs_dgrad else None
             elif isinstance(op, _ActOp):
                 op.dz = e(B, o.H, o.W, o.C) if (op.res_act is not None or op.res_conv is not None) else None
                 # residual BN + ReLU: one mask bit per element replaces re-reading `out` in backward
@@ -369,16 +374,19 @@ class TrunkEngine:
                 dy = op.out.g
                 M = B * op.Ho * op.Wo
                 dres, dx = None, None
+                final = True   # dx is the complete gradient of op.src
                 if op.needs_dgrad:
                     src = op.src
-                    if src.pending is not None and src.g is not None and src.pending is not src.g:
-                        # a residual contribution is waiting: fuse it into this dgrad's epilogue
+                    if src.pending is not None and src.g is not None:
+                        # a contribution is waiting: fuse it into this dgrad's epilogue (in
+                        # place when it already sits in src.g: dres == dx)
                         dres, dx = src.pending, src.g
                         src.pending = None
                     elif src.pending is None and self._has_later_consumer(op):
-                        # first of two contributions (downsample branch): park it in op.dres
-                        dx = op.dres
-                        src.pending = op.dres
+                        # first of two contributions (conv1; the downsample conv adds to it)
+                        dx = src.g
+                        src.pending = src.g
+                        final = False
                     else:
                         dx = src.g
                 if op.conv.bias is not None:   # before conv_done(op) can mark the bucket ready
@@ -389,7 +397,7 @@ class TrunkEngine:
                 args = (dt, op.src.t, dy, op.wt, dres, dx, dw, acc, ws, ws.numel() * 4, B, op.H, op.W, op.cin_pad,
                         op.cin, op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo)
                 a = op.bn_act
-                if a is not None and op.bn_rows > 0 and dx is op.src.g:
+                if a is not None and op.bn_rows > 0 and final and dx is op.src.g and dres is not dx:
                     # dx is the final dout of BN `a`: its partial sums come out of this epilogue
                     if pending is not None:
                         call("wgrad_reduce", ctypes.addressof(pending), st)

@@ -176,7 +176,9 @@ int pose6d_conv2d_fwd(int32_t dtype, const void *x, const void *wp, const float 
 int pose6d_conv_variant(int32_t dtype, int32_t pass, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout,
                         int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo);
 int pose6d_wgrad_variant(int32_t dtype, int32_t M, int32_t Cout, int32_t K, int32_t Cin);
-/* data gradient: dx [N][H][W][Cin] = conv_transpose(dy [N][Ho][Wo][Cout], wt) (+ dres if non-NULL) */
+/* data gradient: dx [N][H][W][Cin] = conv_transpose(dy [N][Ho][Wo][Cout], wt) (+ dres if non-NULL).
+ * dres may be dx itself (accumulate in place); a stride-2 1x1 conv then writes only the
+ * pixels its taps reach (the other three parity classes are left as they are). */
 int pose6d_conv2d_dgrad(int32_t dtype, const void *dy, const void *wt, const void *dres, void *dx, int32_t N,
                         int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
                         int32_t pad, int32_t Ho, int32_t Wo, void *stream);

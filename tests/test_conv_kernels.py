@@ -174,6 +174,17 @@ def test_conv_fast_variants_bit_identical(cfg, monkeypatch):
         assert torch.equal(dxf.cpu(), dx0), f"fused backward dx differs (separate={sep})"
         assert torch.equal(dwf.cpu(), dw0), f"fused backward dw differs (separate={sep})"
     monkeypatch.delenv("POSE6D_BWD_SEPARATE", raising=False)
+    # residual accumulated in place (dres is dx, as the trunk adds the downsample
+    # conv's data gradient to conv1's): same bits as the out-of-place sum
+    dxi = dres.clone()
+    dwi = torch.empty(Cout, Cin, k, k, device=dev)
+    call("conv2d_backward", dt, x, dy, wt, dxi, dxi, dwi, 0, ws, ws.numel() * 4, N, H, W, Cin, Cin, Cout, k, k, s, p,
+         Ho, Wo, stream())
+    dxd = dres.clone()
+    call("conv2d_dgrad", dt, dy, wt, dxd, dxd, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dxi.cpu(), dx0), "in-place backward dx differs"
+    assert torch.equal(dxd.cpu(), dx0), "in-place dgrad differs"
     # the register-staged weight gradient sums the pixels in other splits: close, not equal
     for key in keys:
         monkeypatch.delenv(key, raising=False)

@@ -45,13 +45,14 @@ def main():
     ap.add_argument("--tiles", default="auto,0,1,3")
     ap.add_argument("--stages", default="auto", help="fast-path LDS ring depths to sweep, e.g. auto,2,3,4,6")
     ap.add_argument("--wgrad-env", default="", help="';'-separated K=V[,K=V] settings to sweep for wgrad")
+    ap.add_argument("--env", default="", help="';'-separated K=V[,K=V] settings to sweep for fwd / dgrad")
     ap.add_argument("--B", type=int, default=32)
-    ap.add_argument("--only", type=int, default=-1, help="index into SHAPES")
+    ap.add_argument("--only", default="", help="comma-separated indices into SHAPES")
     a = ap.parse_args()
     B, dt, dtype, dev = a.B, DTYPES[torch.bfloat16], torch.bfloat16, "cuda"
     st = stream()
     tot = {}
-    for (H, W, Cin, Cout, k, s, p) in (SHAPES if a.only < 0 else [SHAPES[a.only]]):
+    for (H, W, Cin, Cout, k, s, p) in (SHAPES if not a.only else [SHAPES[int(i)] for i in a.only.split(",")]):
         Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         x = torch.randn(B, H, W, Cin, device=dev).to(dtype)
         w = torch.randn(Cout, Cin, k, k, device=dev) * 0.05
@@ -68,23 +69,31 @@ def main():
         fns = {
             "fwd": lambda: call("conv2d_fwd", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, st),
             "dgrad": lambda: call("conv2d_dgrad", dt, dy, wt, None, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, st),
+            "dgradip": lambda: call("conv2d_dgrad", dt, dy, wt, dx, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, st),
+            "bwdip": lambda: call("conv2d_backward", dt, x, dy, wt, dx, dx, dw, 0, ws, ws.numel() * 4, B, H, W, Cin,
+                                  Cin, Cout, k, k, s, p, Ho, Wo, st),
+            "bwd": lambda: call("conv2d_backward", dt, x, dy, wt, None, dx, dw, 0, ws, ws.numel() * 4, B, H, W, Cin,
+                                Cin, Cout, k, k, s, p, Ho, Wo, st),
             "wgrad": lambda: call("conv2d_wgrad", dt, x, dy, dw, 0, ws, ws.numel() * 4, B, H, W, Cin, Cin, Cout, k, k,
                                   s, p, Ho, Wo, st),
         }
         line = f"{H:3d}x{W:<3d} {Cin:4d}->{Cout:<4d} k{k}s{s} |"
         for ps in a.passes.split(","):
-            if ps == "wgrad" and a.wgrad_env:
-                for spec in ["auto"] + a.wgrad_env.split(";"):
+            if ps in ("dgrad", "bwd", "dgradip", "bwdip") and Cin % 8:
+                continue   # the stem has no data gradient
+            sweep = a.wgrad_env if ps == "wgrad" else a.env
+            if sweep:
+                for spec in ["auto"] + sweep.split(";"):
                     kv = [] if spec == "auto" else [e.split("=") for e in spec.split(",")]
                     for k_, v_ in kv:
                         os.environ[k_] = v_
                     sec = timeit(fns[ps])
                     for k_, _ in kv:
                         os.environ.pop(k_, None)
-                    line += f" w[{spec}]:{sec * 1e6:6.1f}us/{flops / sec / 1e12:5.0f}T"
+                    line += f" {ps[0]}[{spec}]:{sec * 1e6:6.1f}us/{flops / sec / 1e12:5.0f}T"
                 continue
-            impls = a.impls.split(",") if ps != "wgrad" else ["base"]
-            tiles = a.tiles.split(",") if ps != "wgrad" else ["auto"]
+            impls = {"wgrad": ["base"], "bwd": ["fast"], "bwdip": ["fast"]}.get(ps, a.impls.split(","))
+            tiles = a.tiles.split(",") if ps not in ("wgrad", "bwd", "bwdip") else ["auto"]
             for impl in impls:
                 stages = a.stages.split(",") if impl == "fast" else ["auto"]
                 for t in tiles:

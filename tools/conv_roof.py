@@ -11,11 +11,11 @@ def resnet50_convs():
         for b in range(nb):
             st = s if b == 0 else 1
             Ho = H // st
+            if b == 0:   # the trunk's forward order: downsample first (pose6d/trunk.py)
+                convs.append((f"l{li + 1}.{b}.ds", H, cin, 4 * w, 1, st, Ho))
             convs.append((f"l{li + 1}.{b}.c1", H, cin, w, 1, 1, H))
             convs.append((f"l{li + 1}.{b}.c2", H, w, w, 3, st, Ho))
             convs.append((f"l{li + 1}.{b}.c3", Ho, w, 4 * w, 1, 1, Ho))
-            if b == 0:
-                convs.append((f"l{li + 1}.{b}.ds", H, cin, 4 * w, 1, st, Ho))
             cin, H = 4 * w, Ho
     return convs
 

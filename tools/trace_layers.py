@@ -27,20 +27,14 @@ def main():
     B = 32
     fwd = conv[:len(convs)]
     bwd = conv[len(convs):]
-    # backward issue order: reversed trunk ops -> per block: ds, c3, c2, c1
+    # backward issue order: reversed trunk ops -> per block: c3, c2, c1, ds
     order = []
-    i = len(convs) - 1
-    blocks = []
-    cur = []
+    blocks = {}
     for c in convs[1:]:
-        if c[0].endswith(".c1") and cur:
-            blocks.append(cur)
-            cur = []
-        cur.append(c)
-    blocks.append(cur)
-    for blk in reversed(blocks):
+        blocks.setdefault(c[0].rsplit(".", 1)[0], []).append(c)
+    for blk in reversed(list(blocks.values())):
         names = {c[0].rsplit(".", 1)[1]: c for c in blk}
-        for k in ("ds", "c3", "c2", "c1"):
+        for k in ("c3", "c2", "c1", "ds"):
             if k in names:
                 order.append(names[k])
     order.append(convs[0])
