@@ -701,7 +701,9 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
     }
   }
   const unsigned ring_base = lds_addr(smem);
-  auto compute = [&](int buf) {
+  // mid(): issued between the fragment reads and their wait, so the next stage's
+  // LDS-DMA issue (tens of cycles per instruction) overlaps the LDS read latency
+  auto compute = [&](int buf, auto&& mid) {
     const unsigned slot = ring_base + buf * STAGE;
     if constexpr (TM + TN == 4 && kPairedFrags) {
       unsigned addr[2][4];
@@ -711,6 +713,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
         for (int r = 0; r < 4; ++r) addr[kk][r] = slot + frag_off[kk][r];
       u32x4 f[2][4];
       lds_issue_frags8(f, addr);
+      mid();
       lds_wait_first(f[0]);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -725,6 +728,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
       }
       return;
     }
+    mid();
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       unsigned addr[TM + TN];
@@ -748,8 +752,9 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
   for (int kt = 0; kt < nk; ++kt) {
     const int left = nk - 1 - kt;
     wait_ahead<LOADS, S - 2>(left < S - 2 ? left : S - 2);   // stage kt landed, for every wave
-    if (kt + S - 1 < nk) issue(kt + S - 1, wbuf);
-    compute(cur);
+    compute(cur, [&]() {
+      if (kt + S - 1 < nk) issue(kt + S - 1, wbuf);
+    });
     cur = cur == S - 1 ? 0 : cur + 1;
     wbuf = wbuf == S - 1 ? 0 : wbuf + 1;
   }

@@ -63,6 +63,21 @@ __device__ __forceinline__ void lds_read_tr_frags(u32x2 (&f)[2 * NF], const unsi
   }
 }
 
+// the 4-operand batch without its wait (lds_wait_tr8 releases it), so other work
+// can be issued while the reads are in flight
+__device__ __forceinline__ void lds_issue_tr8(u32x2 (&f)[8], const unsigned (&a)[8]) {
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %8\n\tds_read_b64_tr_b16 %1, %9\n\tds_read_b64_tr_b16 %2, %10\n\t"
+      "ds_read_b64_tr_b16 %3, %11\n\tds_read_b64_tr_b16 %4, %12\n\tds_read_b64_tr_b16 %5, %13\n\t"
+      "ds_read_b64_tr_b16 %6, %14\n\tds_read_b64_tr_b16 %7, %15"
+      : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]), "=&v"(f[4]), "=&v"(f[5]), "=&v"(f[6]), "=&v"(f[7])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]));
+}
+__device__ __forceinline__ void lds_wait_tr8(u32x2 (&f)[8]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7]));
+}
+
 // one workgroup's work; `bid` = its index in the weight-gradient sub-grid (whose
 // size is a multiple of 8 or the whole grid, so bid & 7 is its XCD), `smem` = the
 // kernel's dynamic LDS
@@ -186,7 +201,8 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
         off[kk][2 * o + h] = sub * SUB + r * 128 + (((lc >> 3) ^ swz_tr4(r)) << 4) + (lc & 7) * 2;
       }
   const unsigned ring = lds_addr(smem);
-  auto compute = [&](int buf) {
+  // mid(): the next stage's LDS-DMA issue, placed while the first fragment batch is in flight
+  auto compute = [&](int buf, auto&& mid) {
     const unsigned slot = ring + buf * STAGE;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -198,8 +214,20 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
         u32x2 t[2 * NB];
 #pragma unroll
         for (int u = 0; u < 2 * NB; ++u) a[u] = slot + off[kk][2 * b0 + u];
-        if constexpr (NB == 4) lds_read_tr_frags<4>(t, a);
-        else lds_read_tr_frags<2>(t, a);
+        if (kk == 0 && b0 == 0) {
+          if constexpr (NB == 4) {
+            lds_issue_tr8(t, a);
+            mid();
+            lds_wait_tr8(t);
+          } else {
+            mid();
+            lds_read_tr_frags<2>(t, a);
+          }
+        } else if constexpr (NB == 4) {
+          lds_read_tr_frags<4>(t, a);
+        } else {
+          lds_read_tr_frags<2>(t, a);
+        }
 #pragma unroll
         for (int u = 0; u < 2 * NB; ++u) f[2 * b0 + u] = t[u];
       }
@@ -221,8 +249,9 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
   for (int kt = 0; kt < nk; ++kt) {
     const int left = nk - 1 - kt;
     wait_ahead<LOADS, S - 2>(left < S - 2 ? left : S - 2);
-    if (kt + S - 1 < nk) issue(kt + S - 1, wbuf);
-    compute(cur);
+    compute(cur, [&]() {
+      if (kt + S - 1 < nk) issue(kt + S - 1, wbuf);
+    });
     cur = cur == S - 1 ? 0 : cur + 1;
     wbuf = wbuf == S - 1 ? 0 : wbuf + 1;
   }
