@@ -162,7 +162,7 @@ def main():
         result.update(kernel_profile(tr, ms))
     if rank == 0 and not args.no_side:
         result["side_configs"] = {"configs[1]": rgb_fp32_forward(dev), "configs[3]": add_eval_throughput(dev),
-                                  "frame_crops": crop_throughput(dev)}
+                                  "frame_crops": crop_throughput(dev), "inference_b1": inference_latency(dev)}
     if rank == 0 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline()
@@ -311,6 +311,33 @@ def crop_throughput(dev, B=32, reps=20):
             "value": round(B / t, 1), "unit": "crops/s", "ms_per_batch": round(t * 1e3, 4), "dtype": "u8/u16->f32",
             "hbm_roofline": {"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_bytes_per_batch": round(nbytes)}}
+
+
+def inference_latency(dev, reps=50):
+    """single-image inference (inference_*.py calls the model on one
+    detected crop at a time): PoseNetRGBDGeometric eval forward at B=1, 224^2, with
+    the pinhole translation -- latency per call, eager (one Python call of the drop-in
+    module) and replayed from a captured hipGraph; fp32 (reference numerics) and bf16."""
+    from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
+    torch.manual_seed(0)
+    out = {"workload": "PoseNetRGBDGeometric eval forward, B=1, 224^2 (+ pinhole translation)", "unit": "ms"}
+    b = synth_batch(1, dev, seed=0)
+    args = (b[0], None, b[1], b[2], b[3])
+    for name, dt in (("f32", torch.float32), ("bf16", torch.bfloat16)):
+        m = PoseNetRGBDGeometric(pretrained=False).to(dev).set_compute_dtype(dt).eval()
+        with torch.no_grad():
+            eager = _time_fn(lambda: m(*args), reps)
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                m(*args)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                m(*args)
+            graph = _time_fn(g.replay, reps)
+        out[name] = {"eager_ms": round(eager * 1e3, 4), "graph_ms": round(graph * 1e3, 4)}
+    return out
 
 
 def forward_time(tr, reps=20):

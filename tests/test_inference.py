@@ -1,0 +1,39 @@
+"""Single-image inference (the reference's inference_*.py call the
+model on one crop at a time): B=1 eval forward of every model against the oracle,
+and the same forward captured into a hipGraph and replayed (the latency path
+bench.py's `inference_b1` times) giving the eager result bit for bit."""
+import pytest
+import torch
+
+from tests.test_models import EXPECTED, _close, _inputs, _model_forward, _oracle_run, _models
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", list(EXPECTED))
+def test_b1_eval_forward_and_graph_replay(name):
+    torch.manual_seed(0)
+    m = _models()[name](pretrained=False)
+    P0 = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.cuda().eval()
+    g = torch.Generator().manual_seed(3)
+    inp = _inputs(1, 224, g)
+    cin = {k: v.cuda() for k, v in inp.items()}
+    with torch.no_grad():
+        rot, trans = _model_forward(name, m, cin)
+        rr, tr, _, _ = _oracle_run(name, P0, inp, False, torch.float32)
+        _close(rot, rr, 1e-4, "rotation")
+        _close(trans, tr, 1e-4, "translation")
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            _model_forward(name, m, cin)
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            grot, gtrans = _model_forward(name, m, cin)
+        cin["rgb"].copy_(torch.randn(1, 3, 224, 224, generator=g).cuda())   # new crop, same buffers
+        graph.replay()
+        rot2, trans2 = _model_forward(name, m, cin)
+        torch.cuda.synchronize()
+    assert torch.equal(grot, rot2) and torch.equal(gtrans, trans2)
