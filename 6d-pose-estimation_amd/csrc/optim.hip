@@ -15,9 +15,16 @@ namespace {
 
 constexpr int kThreads = 256;
 
+// `step` / `seed` (optional): the trainer's device step counter (hp[5]) and dropout
+// seed word, advanced here so the captured step needs no launches of its own for them
 __global__ __launch_bounds__(kThreads) void sumsq_kernel(const float* __restrict__ g, int64_t n,
-                                                         float* __restrict__ part) {
+                                                         float* __restrict__ part, float* __restrict__ step,
+                                                         int64_t* __restrict__ seed) {
   __shared__ float red[kThreads / 64];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (step) step[0] += 1.f;
+    if (seed) seed[0] += 1;
+  }
   float s = 0.f;
   const int64_t n4 = n / 4;
   const float4* g4 = reinterpret_cast<const float4*>(g);
@@ -83,7 +90,15 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float* __restrict__ p, 
 
 extern "C" int pose6d_sumsq_partial(const float* g, int64_t n, float* partials, int32_t nparts, void* stream) {
   P6_CHECK_ARG(nparts > 0 && nparts <= 65535, "pose6d_sumsq_partial: bad nparts");
-  sumsq_kernel<<<nparts, kThreads, 0, p6::stream_of(stream)>>>(g, n, partials);
+  sumsq_kernel<<<nparts, kThreads, 0, p6::stream_of(stream)>>>(g, n, partials, nullptr, nullptr);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+extern "C" int pose6d_sumsq_partial_step(const float* g, int64_t n, float* partials, int32_t nparts, float* step,
+                                         int64_t* seed, void* stream) {
+  P6_CHECK_ARG(nparts > 0 && nparts <= 65535, "pose6d_sumsq_partial_step: bad nparts");
+  sumsq_kernel<<<nparts, kThreads, 0, p6::stream_of(stream)>>>(g, n, partials, step, seed);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }

@@ -132,11 +132,12 @@ class RGBDGeometricTrainer:
         st = stream()
         if self.world > 1:
             self.arena.grad.mul_(1.0 / self.world)
-        self.hp[5:6].add_(1.0)
-        call("sumsq_partial", self.arena.grad, self.arena.numel, self.partials, NPART, st)
+        # step counter hp[5] += 1 and dropout seed += 1 ride on the norm-partials launch
+        # (the seed is next read by the following step's forward)
+        call("sumsq_partial_step", self.arena.grad, self.arena.numel, self.partials, NPART,
+             self.hp[5:6], self.seed, st)
         call("adamw_step", self.arena.flat, self.arena.grad, self.m, self.v, self.arena.numel, self.partials, NPART,
              self.hp, self.norm, st)
-        self.seed.add_(1)
 
     def step_eager(self, data):
         """One training step without graphs (reference order of operations)."""

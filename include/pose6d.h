@@ -382,6 +382,10 @@ int pose6d_xattn_bwd(const float *dout, const float *q, const float *k, const fl
  *                max_norm (<= 0: no clipping)}
  * ---------------------------------------------------------------------- */
 int pose6d_sumsq_partial(const float *g, int64_t n, float *partials, int32_t nparts, void *stream);
+/* the same, and (each optional) step[0] += 1 (the hp[5] counter pose6d_adamw_step reads next) and
+ * seed[0] += 1 (the trainer's dropout seed word): the per-step counters without launches of their own */
+int pose6d_sumsq_partial_step(const float *g, int64_t n, float *partials, int32_t nparts, float *step,
+                              int64_t *seed, void *stream);
 int pose6d_adamw_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
                       const float *partials, int32_t nparts, const float *hp, float *norm_out, void *stream);
 
