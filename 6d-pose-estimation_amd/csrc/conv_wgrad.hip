@@ -278,7 +278,10 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC) {
     p.stages = env_int("POSE6D_WGRAD_STAGES", 3);
     if (p.stages < 2) p.stages = 2;
     if (p.stages > 4) p.stages = 4;
-    target = env_int("POSE6D_WGRAD_BLOCKS", 1024);
+    // ~640 workgroups: fewer fp32 slabs to write and reduce than 1024, still ~2.5 per
+    // CU beside the data-gradient workgroups of the fused launch (end-to-end sweep:
+    // 384 / 512 / 640 / 1024 -> 5.24 / 5.16 / 5.14 / 5.20 ms per step)
+    target = env_int("POSE6D_WGRAD_BLOCKS", 640);
     min_rows = 256;
     step = 64;
     max_bytes = 48ll << 20;
