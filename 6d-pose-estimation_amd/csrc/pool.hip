@@ -210,6 +210,64 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, u
   }
 }
 
+// BatchNorm-apply + ReLU + max pool in one pass (the stem / z-CNN act -> pool pairs):
+// the pool reads the raw conv output y and forms each window element exactly as
+// pose6d_bn_act_fwd would have stored it, T(max(y * scale + shift, 0)), so the pooled
+// values and argmax equal bn_act_fwd followed by maxpool_fwd bit for bit -- without
+// writing and re-reading the full-resolution activation (nothing else reads it: the
+// backward recomputes the ReLU sign from y and routes the pool gradient by argmax).
+template <typename T>
+__global__ void bn_relu_maxpool_fwd_kernel(const T* __restrict__ x, const float* __restrict__ scale,
+                                           const float* __restrict__ shift, T* __restrict__ y,
+                                           uint8_t* __restrict__ idx, int N, int H, int W, int C, int Ho, int Wo,
+                                           int k, int s, int p) {
+  constexpr int E = V<T>::E;
+  const int cpr = C / E;
+  const int i = blockIdx.x * kThreads + threadIdx.x;  // (column, chunk) within the output row
+  if (i >= Wo * cpr) return;
+  const int n = blockIdx.y / Ho, oy = blockIdx.y - n * Ho;
+  const int ox = i / cpr, c0 = (i - ox * cpr) * E;
+  const int64_t pix = ((int64_t)n * Ho + oy) * Wo + ox;
+  float sc[E], sh[E], best[E];
+  uint8_t bi[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    sc[e] = scale[c0 + e];
+    sh[e] = shift[c0 + e];
+    best[e] = -__builtin_inff();
+    bi[e] = 0;
+  }
+  bool first = true;
+  for (int kh = 0; kh < k; ++kh) {
+    const int iy = oy * s - p + kh;
+    if (iy < 0 || iy >= H) continue;
+    for (int kw = 0; kw < k; ++kw) {
+      const int ix = ox * s - p + kw;
+      if (ix < 0 || ix >= W) continue;
+      float v[E];
+      ld(x + (((int64_t)n * H + iy) * W + ix) * C + c0, v);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        v[e] = p6::to_f(p6::from_f<T>(fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f)));
+        if (first || v[e] > best[e] || v[e] != v[e]) { best[e] = v[e]; bi[e] = (uint8_t)(kh * k + kw); }
+      }
+      first = false;
+    }
+  }
+  st(y + pix * C + c0, best);
+  if (idx) {
+    if constexpr (E == 8) {
+      uint2 u;
+      __builtin_memcpy(&u, bi, 8);
+      *reinterpret_cast<uint2*>(idx + pix * C + c0) = u;
+    } else {
+      uint32_t u;
+      __builtin_memcpy(&u, bi, 4);
+      *reinterpret_cast<uint32_t*>(idx + pix * C + c0) = u;
+    }
+  }
+}
+
 template <typename T>
 __global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx, T* __restrict__ dx, int N,
                                    int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
@@ -355,6 +413,26 @@ extern "C" int pose6d_maxpool_fwd(int32_t dtype, const void* x, void* y, uint8_t
   else
     maxpool_fwd_kernel<float><<<grid, kThreads, 0, st_>>>((const float*)x, (float*)y, argmax, N, H, W, C, Ho, Wo, k, s,
                                                           p);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+extern "C" int pose6d_bn_relu_maxpool_fwd(int32_t dtype, const void* x, const float* scale, const float* shift,
+                                          void* y, uint8_t* argmax, int32_t N, int32_t H, int32_t W, int32_t C,
+                                          int32_t k, int32_t s, int32_t p, int32_t Ho, int32_t Wo, void* stream) {
+  P6_CHECK_ARG(k * k <= 255, "pose6d_bn_relu_maxpool_fwd: window too large");
+  P6_CHECK_ARG(scale && shift, "pose6d_bn_relu_maxpool_fwd: null scale / shift");
+  P6_POOL_CHECK(C, dtype);
+  hipStream_t st_ = p6::stream_of(stream);
+  if ((int64_t)N * Ho * Wo == 0) return POSE6D_OK;
+  const int E = dtype == POSE6D_DT_BF16 ? 8 : 4;
+  const dim3 grid(p6::ceil_div((int64_t)Wo * (C / E), kThreads), N * Ho);
+  if (dtype == POSE6D_DT_BF16)
+    bn_relu_maxpool_fwd_kernel<bf16><<<grid, kThreads, 0, st_>>>((const bf16*)x, scale, shift, (bf16*)y, argmax, N, H,
+                                                                 W, C, Ho, Wo, k, s, p);
+  else
+    bn_relu_maxpool_fwd_kernel<float><<<grid, kThreads, 0, st_>>>((const float*)x, scale, shift, (float*)y, argmax, N,
+                                                                  H, W, C, Ho, Wo, k, s, p);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }

@@ -87,11 +87,13 @@ class _ActOp:
     def __init__(self, cop, relu, res_act=None, res_conv=None, name=""):
         self.cop, self.relu, self.res_act, self.res_conv = cop, relu, res_act, res_conv
         self.out = _Act(cop.cout, cop.Ho, cop.Wo, name)
+        self.pooled = False   # applied inside the following max pool (its output is never stored)
 
 
 class _PoolOp:
     def __init__(self, src, k, s, p, name):
         self.src, self.k, self.s, self.p = src, k, s, p
+        self.act = None   # the plain BN+ReLU this pool applies on the fly (pose6d_bn_relu_maxpool_fwd)
         Ho = (src.H + 2 * p - k) // s + 1
         Wo = (src.W + 2 * p - k) // s + 1
         self.out = _Act(src.C, Ho, Wo, name)
@@ -168,6 +170,14 @@ class TrunkEngine:
             self.final = cur
         else:
             raise ValueError(self.kind)
+        # act -> pool pairs whose activation feeds only the pool (stem, z-CNN): one pass
+        for i, op in enumerate(self.ops[:-1]):
+            nxt = self.ops[i + 1]
+            if (isinstance(op, _ActOp) and isinstance(nxt, _PoolOp) and nxt.src is op.out and op.relu
+                    and op.res_act is None and op.res_conv is None
+                    and not any(o is not nxt and (getattr(o, "src", None) is op.out
+                                                  or getattr(o, "res_act", None) is op.out) for o in self.ops)):
+                op.pooled, nxt.act = True, op
         self.feat_dim = self.final.C
 
     # ------------------------------------------------------------ allocation
@@ -293,6 +303,8 @@ class TrunkEngine:
                      float(bn.momentum if bn.momentum is not None else 0.1), float(bn.eps), int(training),
                      op.scale, op.shift, op.mean, op.inv, self.ws_fin, st)
             elif isinstance(op, _ActOp):
+                if op.pooled:
+                    continue   # applied by the following pool
                 c = op.cop
                 M = B * c.Ho * c.Wo
                 mb = op.mbits if training else None
@@ -303,6 +315,10 @@ class TrunkEngine:
                 else:
                     call("bn_act_fwd_mask", dt, c.out.t, c.scale, c.shift, op.res_act.t if op.res_act else None, None,
                          None, int(op.relu), op.out.t, mb, M, c.cout, st)
+            elif op.act is not None:
+                s, c = op.src, op.act.cop
+                call("bn_relu_maxpool_fwd", dt, c.out.t, c.scale, c.shift, op.out.t, op.argmax, B, s.H, s.W, s.C,
+                     op.k, op.s, op.p, op.out.H, op.out.W, st)
             else:
                 s = op.src
                 call("maxpool_fwd", dt, s.t, op.out.t, op.argmax, B, s.H, s.W, s.C, op.k, op.s, op.p, op.out.H,

@@ -300,6 +300,11 @@ int pose6d_channel_sum(int32_t dtype, const void *x, int64_t M, int32_t C, float
 /* nn.MaxPool2d(k, s, p) on NHWC; argmax = window index (uint8) of the first max */
 int pose6d_maxpool_fwd(int32_t dtype, const void *x, void *y, uint8_t *argmax, int32_t N, int32_t H, int32_t W,
                        int32_t C, int32_t k, int32_t s, int32_t p, int32_t Ho, int32_t Wo, void *stream);
+/* pose6d_bn_act_fwd (ReLU, no residual) followed by pose6d_maxpool_fwd in one pass: y, argmax
+ * as that pair would produce them (bit for bit), without the full-resolution activation. */
+int pose6d_bn_relu_maxpool_fwd(int32_t dtype, const void *x, const float *scale, const float *shift, void *y,
+                               uint8_t *argmax, int32_t N, int32_t H, int32_t W, int32_t C, int32_t k, int32_t s,
+                               int32_t p, int32_t Ho, int32_t Wo, void *stream);
 int pose6d_maxpool_bwd(int32_t dtype, const void *dy, const uint8_t *argmax, void *dx, int32_t N, int32_t H,
                        int32_t W, int32_t C, int32_t k, int32_t s, int32_t p, int32_t Ho, int32_t Wo, void *stream);
 /* nn.AdaptiveAvgPool2d(1) + view(B, -1): x [N][HW][C] -> y [N][C] fp32 */

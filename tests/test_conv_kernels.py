@@ -308,6 +308,18 @@ def test_pools(dtype):
         dx = torch.empty_like(xd)
         call("maxpool_bwd", dt, _nhwc(dy).to(dev, dtype), am, dx, N, H, W, C, k, s, p, Ho, Wo, stream())
         _close(dx.permute(0, 3, 1, 2), xr.grad, 1e-6 if dtype == torch.float32 else 1e-2, "maxpool bwd")
+        # BN-apply + ReLU + pool in one pass == bn_act_fwd then maxpool_fwd, bit for bit
+        yraw = _nhwc(torch.randn(N, C, H, W, generator=g)).to(dev, dtype)
+        sc = (torch.rand(C, generator=g) + 0.5).to(dev)
+        sh = (torch.randn(C, generator=g) * 0.5).to(dev)
+        act = torch.empty_like(yraw)
+        call("bn_act_fwd", dt, yraw, sc, sh, None, None, None, 1, act, N * H * W, C, stream())
+        y1, a1 = torch.empty_like(y), torch.empty_like(am)
+        call("maxpool_fwd", dt, act, y1, a1, N, H, W, C, k, s, p, Ho, Wo, stream())
+        y2, a2 = torch.empty_like(y), torch.empty_like(am)
+        call("bn_relu_maxpool_fwd", dt, yraw, sc, sh, y2, a2, N, H, W, C, k, s, p, Ho, Wo, stream())
+        torch.cuda.synchronize()
+        assert torch.equal(y1, y2) and torch.equal(a1, a2)
     x = torch.randn(2, 64, 7, 7, generator=g)
     f = torch.empty(2, 64, device=dev)
     call("avgpool_fwd", 0, _nhwc(x).to(dev), f, 2, 49, 64, stream())
