@@ -231,6 +231,27 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_kernel(
   }
 }
 
+// ---------------------------------------------------------------- eval fold (all BNs, one launch)
+// the eval branch of bn_finalize_kernel for a table of BatchNorms (pose6d_bn_eval_fold)
+struct EvalFold {
+  const float *gamma, *beta, *rmean, *rvar;
+  float *scale, *shift, *smean, *sinv;
+  float eps;
+  int32_t C;
+};
+static_assert(sizeof(EvalFold) == 72, "pose6d_bn_fold_t layout");
+__global__ __launch_bounds__(kThreads) void bn_eval_fold_kernel(const EvalFold* __restrict__ d) {
+  const EvalFold f = d[blockIdx.y];
+  for (int c = blockIdx.x * kThreads + threadIdx.x; c < f.C; c += gridDim.x * kThreads) {
+    const float inv = 1.0f / sqrtf(f.rvar[c] + f.eps);
+    const float sc = f.gamma[c] * inv;
+    f.scale[c] = sc;
+    f.shift[c] = f.beta[c] - f.rmean[c] * sc;
+    f.smean[c] = f.rmean[c];
+    f.sinv[c] = inv;
+  }
+}
+
 // ---------------------------------------------------------------- apply fwd
 template <typename T>
 __global__ __launch_bounds__(kThreads) void bn_act_kernel(const T* __restrict__ y, const float* __restrict__ scale,
@@ -482,6 +503,17 @@ int rows_per_block(int64_t M) {
 }
 
 }  // namespace
+
+extern "C" int pose6d_bn_fold_desc_size(void) { return (int)sizeof(EvalFold); }
+
+extern "C" int pose6d_bn_eval_fold(const void* descs, int32_t n, int32_t max_c, void* stream) {
+  P6_CHECK_ARG(n >= 0 && n <= 65535 && max_c >= 0, "pose6d_bn_eval_fold: bad table size");
+  if (n == 0 || max_c == 0) return POSE6D_OK;
+  bn_eval_fold_kernel<<<dim3(p6::ceil_div(max_c, kThreads), n), kThreads, 0, p6::stream_of(stream)>>>(
+      (const EvalFold*)descs);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
 
 extern "C" int pose6d_bn_finalize(const float* partial, int32_t rows, int32_t C, int64_t count, const float* gamma,
                                   const float* beta, float* running_mean, float* running_var, int64_t* num_batches,

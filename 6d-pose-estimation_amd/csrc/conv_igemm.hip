@@ -45,6 +45,11 @@ struct Geom {
   int gm, gn;              // grid in tiles
   int nmajor;              // fast path: tile order N-major (weights larger than the gathered source)
   int s2one;               // kDgradS2: 0 = grid covers the four parity classes; c + 1 = only class c
+  // forward with the BatchNorm already known (eval): the epilogue stores
+  // act(T(y) * scale + shift [+ res | + res * res_scale + res_shift]) instead of y
+  // (pose6d_conv2d_fwd_act); `res` is then the residual tensor
+  const float *act_scale, *act_shift, *act_rscale, *act_rshift;
+  int act, act_relu;
 };
 
 // kDgradS2 launched in place (dres == dx) when a single parity class has taps
@@ -199,6 +204,21 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], ch
   float bs[E], bq[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) bs[e] = bq[e] = 0.f;
+  // eval BN-act: a thread's 16-B chunk column (tid % CPR) is the same on every store
+  // iteration, so its channels' constants are loaded once
+  static_assert(kThreads % CPR == 0, "store loop: fixed chunk column per thread");
+  float asc[E], ash[E], arsc[E], arsh[E];
+  if (g.act) {
+    const int c = n0 + (tid % CPR) * E;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const bool ok = c + e < g.Ncols;
+      asc[e] = ok ? g.act_scale[c + e] : 0.f;
+      ash[e] = ok ? g.act_shift[c + e] : 0.f;
+      arsc[e] = ok && g.act_rscale ? g.act_rscale[c + e] : 0.f;
+      arsh[e] = ok && g.act_rscale ? g.act_rshift[c + e] : 0.f;
+    }
+  }
 #pragma unroll
   for (int it = 0; it < (BM * CPR + kThreads - 1) / kThreads; ++it) {
     const int idx = tid + it * kThreads;
@@ -209,7 +229,23 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], ch
     uint4 v = *reinterpret_cast<const uint4*>(smem + lr * CROW + cc * 16);
     const int64_t om = out_row(g, cls, m);
     T* dst = out + om * g.Ncols + c;
-    if (res) {
+    if (g.act) {
+      // pose6d_bn_act_fwd's arithmetic on the stored (T-rounded) conv output
+      T a[E], b[E];
+      __builtin_memcpy(a, &v, 16);
+      if (res) {
+        const uint4 rv = *reinterpret_cast<const uint4*>(res + om * g.Ncols + c);
+        __builtin_memcpy(b, &rv, 16);
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        float x = fmaf(p6::to_f(a[e]), asc[e], ash[e]);
+        if (res) x += g.act_rscale ? fmaf(p6::to_f(b[e]), arsc[e], arsh[e]) : p6::to_f(b[e]);
+        if (g.act_relu) x = fmaxf(x, 0.f);
+        a[e] = p6::from_f<T>(x);
+      }
+      __builtin_memcpy(&v, a, 16);
+    } else if (res) {
       const uint4 rv = *reinterpret_cast<const uint4*>(res + om * g.Ncols + c);
       T a[E], b[E];
       __builtin_memcpy(a, &v, 16);
@@ -1048,6 +1084,35 @@ extern "C" int pose6d_conv2d_fwd(int32_t dtype, const void* x, const void* w, co
                  bk, Cin);
   if (mode == kGemm) P6_CHECK_ARG(Cin % bk == 0, "pose6d_conv2d_fwd: 1x1 Cin %% %d != 0", bk);
   return run_conv(dtype, mode, g, x, w, bias, nullptr, y, stats, p6::stream_of(stream));
+}
+
+// eval-mode conv + BatchNorm apply (+ residual, + ReLU) in one launch: the store of
+// pose6d_conv2d_fwd followed by pose6d_bn_act_fwd, bit for bit, without the raw output
+extern "C" int pose6d_conv2d_fwd_act(int32_t dtype, const void* x, const void* w, const float* bias, void* out,
+                                     int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW,
+                                     int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, const float* scale,
+                                     const float* shift, const void* res, const float* res_scale,
+                                     const float* res_shift, int32_t relu, void* stream) {
+  P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_fwd_act: bad dtype %d", dtype);
+  P6_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cout > 0 && Cout % 8 == 0, "pose6d_conv2d_fwd_act: bad shape (Cout %% 8)");
+  P6_CHECK_ARG(Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1,
+               "pose6d_conv2d_fwd_act: Ho/Wo inconsistent");
+  P6_CHECK_ARG(scale && shift, "pose6d_conv2d_fwd_act: null scale / shift");
+  P6_CHECK_ARG(!res_scale == !res_shift && (!res_scale || res), "pose6d_conv2d_fwd_act: bad residual BN args");
+  const int bk = dtype == POSE6D_DT_BF16 ? 32 : 16;
+  int mode;
+  Geom g = fwd_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
+  if (mode == kFwd)
+    P6_CHECK_ARG(g.log2SC >= 0 && Cin % bk == 0,
+                 "pose6d_conv2d_fwd_act: Cin must be 4 or a power of two >= %d (got %d)", bk, Cin);
+  if (mode == kGemm) P6_CHECK_ARG(Cin % bk == 0, "pose6d_conv2d_fwd_act: 1x1 Cin %% %d != 0", bk);
+  g.act = 1;
+  g.act_relu = relu != 0;
+  g.act_scale = scale;
+  g.act_shift = shift;
+  g.act_rscale = res_scale;
+  g.act_rshift = res_shift;
+  return run_conv(dtype, mode, g, x, w, bias, res, out, nullptr, p6::stream_of(stream));
 }
 
 extern "C" int pose6d_conv2d_dgrad(int32_t dtype, const void* dy, const void* wt, const void* dres, void* dx,

@@ -34,6 +34,9 @@ class _WgradReduce(ctypes.Structure):
                                       "Ho", "Wo", "accumulate")]
 
 
+# pose6d_bn_fold_t (include/pose6d.h): eval-mode BN fold table entry
+_FOLD = np.dtype([("gamma", "<u8"), ("beta", "<u8"), ("rmean", "<u8"), ("rvar", "<u8"), ("scale", "<u8"),
+                  ("shift", "<u8"), ("smean", "<u8"), ("sinv", "<u8"), ("eps", "<f4"), ("C", "<i4")])
 _DESC = np.dtype([("w", "<u8"), ("wp", "<u8"), ("wt", "<u8"), ("O", "<i4"), ("I", "<i4"), ("Ip", "<i4"),
                   ("KH", "<i4"), ("KW", "<i4"), ("Kpad", "<i4"), ("start", "<i8"), ("count", "<i8")])
 
@@ -78,6 +81,7 @@ class _ConvOp:
         self.Ho = (self.H + 2 * self.pad - self.k) // self.stride + 1
         self.Wo = (self.W + 2 * self.pad - self.k) // self.stride + 1
         self.out = _Act(self.cout, self.Ho, self.Wo, name + ".y")
+        self.act_op = None   # the _ActOp applying this conv's BN (set by _ActOp)
         self.needs_dgrad = True
 
 
@@ -86,6 +90,7 @@ class _ActOp:
 
     def __init__(self, cop, relu, res_act=None, res_conv=None, name=""):
         self.cop, self.relu, self.res_act, self.res_conv = cop, relu, res_act, res_conv
+        cop.act_op = self   # the BN+act applied to this conv's output
         self.out = _Act(cop.cout, cop.Ho, cop.Wo, name)
         self.pooled = False   # applied inside the following max pool (its output is never stored)
 
@@ -243,10 +248,28 @@ class TrunkEngine:
         self.ws_fin = torch.empty(64 * 3 * max(op.cout for op in self.convs), device=device, dtype=torch.float64)
         self.feat = f32(B, self.feat_dim)
         self.feat_grad_in = None
+        self._fold_dev, self._fold_key = None, None
         # weight packing descriptors (one launch for all convs)
         self._desc_dev = None
         self._pack_key = None
         self._build_pack_table()
+
+    def _eval_fold(self, st):
+        """Eval scale/shift (+ saved mean / invstd) of every BN from its running
+        statistics: ONE launch (pose6d_bn_eval_fold) instead of one per BN."""
+        key = tuple((op.bn.weight.data_ptr(), op.bn.bias.data_ptr(), op.bn.running_mean.data_ptr(),
+                     op.bn.running_var.data_ptr(), float(op.bn.eps)) for op in self.convs)
+        if key != self._fold_key:
+            assert query("bn_fold_desc_size") == _FOLD.itemsize
+            rec = np.zeros(len(self.convs), dtype=_FOLD)
+            for i, op in enumerate(self.convs):
+                bn = op.bn
+                rec[i] = (bn.weight.data_ptr(), bn.bias.data_ptr(), bn.running_mean.data_ptr(),
+                          bn.running_var.data_ptr(), op.scale.data_ptr(), op.shift.data_ptr(), op.mean.data_ptr(),
+                          op.inv.data_ptr(), float(bn.eps), op.cout)
+            self._fold_dev = torch.from_numpy(rec.view(np.uint8).copy()).to(self.device)
+            self._fold_key = key
+        call("bn_eval_fold", self._fold_dev, len(self.convs), max(op.cout for op in self.convs), st)
 
     def _build_pack_table(self):
         n = len(self.convs)
@@ -291,20 +314,38 @@ class TrunkEngine:
             xf = xf.float()
         xf = xf.contiguous()
         call("nchw_to_nhwc", dt, xf, self.input.t, B, C, H, W, self.input.C, st)
+        # eval: the BN (running statistics) is known before the conv runs, so the conv's
+        # epilogue applies BN (+ residual) + ReLU and stores the activation directly
+        fold = not training and os.environ.get("POSE6D_EVAL_FUSE", "1") != "0"
+        if fold:
+            self._eval_fold(st)
         for op in self.ops:
             if isinstance(op, _ConvOp):
                 bias = op.conv.bias
-                call("conv2d_fwd", dt, op.src.t, op.wp, bias.detach() if bias is not None else None, op.out.t,
-                     op.stats if training else None, B, op.H, op.W, op.cin_pad, op.cout, op.k, op.k, op.stride,
-                     op.pad, op.Ho, op.Wo, st)
+                bias = bias.detach() if bias is not None else None
                 bn = op.bn
-                call("bn_finalize", op.stats, op.stats_rows, op.cout, B * op.Ho * op.Wo, bn.weight.detach(),
-                     bn.bias.detach(), bn.running_mean, bn.running_var, bn.num_batches_tracked,
-                     float(bn.momentum if bn.momentum is not None else 0.1), float(bn.eps), int(training),
-                     op.scale, op.shift, op.mean, op.inv, self.ws_fin, st)
+                fin = ("bn_finalize", op.stats, op.stats_rows, op.cout, B * op.Ho * op.Wo, bn.weight.detach(),
+                       bn.bias.detach(), bn.running_mean, bn.running_var, bn.num_batches_tracked,
+                       float(bn.momentum if bn.momentum is not None else 0.1), float(bn.eps), int(training),
+                       op.scale, op.shift, op.mean, op.inv, self.ws_fin, st)
+                a = getattr(op, "act_op", None)
+                if fold and a is not None and not a.pooled:
+                    res, rs, rb = None, None, None
+                    if a.res_conv is not None:
+                        res, rs, rb = a.res_conv.out.t, a.res_conv.scale, a.res_conv.shift
+                    elif a.res_act is not None:
+                        res = a.res_act.t
+                    call("conv2d_fwd_act", dt, op.src.t, op.wp, bias, a.out.t, B, op.H, op.W, op.cin_pad, op.cout,
+                         op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, op.scale, op.shift, res, rs, rb, int(a.relu),
+                         st)
+                    continue
+                call("conv2d_fwd", dt, op.src.t, op.wp, bias, op.out.t, op.stats if training else None, B, op.H,
+                     op.W, op.cin_pad, op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, st)
+                if not fold:
+                    call(*fin)
             elif isinstance(op, _ActOp):
-                if op.pooled:
-                    continue   # applied by the following pool
+                if op.pooled or fold:
+                    continue   # applied by the following pool / by its conv's epilogue
                 c = op.cop
                 M = B * c.Ho * c.Wo
                 mb = op.mbits if training else None

@@ -187,6 +187,9 @@ def kernel_profile(tr, step_ms, with_forward=True):
     # forward-only (training-mode BN) time of the trunk, graph-captured
     fwd_ms = forward_time(tr) if with_forward else float("nan")
     fwd_gbs = FWD_BYTES_PER_CROP * tr.B / (fwd_ms * 1e-3) / 1e9
+    # eval-mode forward of the whole model (BN folded into the conv epilogues), graph-captured
+    ev_ms = eval_forward_time(tr.dev, tr.B) if with_forward else float("nan")
+    ev_gbs = FWD_BYTES_PER_CROP * tr.B / (ev_ms * 1e-3) / 1e9
     pmc, tsrc = pmc_traffic(sym)
     traffic = round(pmc["hbm_bytes_per_launch"]) if pmc else None
     # SQ_VALU_MFMA_BUSY_CYCLES = 16 cycles per 16x16x32 MFMA summed over the chip's
@@ -204,7 +207,14 @@ def kernel_profile(tr, step_ms, with_forward=True):
                       "by_symbol_ms": {k: round(v["time_s"] * 1e3, 3) for k, v in agg.items()}},
         "forward_roofline": {"bound": "hbm", "fwd_ms": round(fwd_ms, 4), "achieved": round(fwd_gbs, 1),
                              "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(fwd_gbs / PEAK_HBM_GBS, 4),
-                             "algorithmic_bytes_per_crop": FWD_BYTES_PER_CROP},
+                             "algorithmic_bytes_per_crop": FWD_BYTES_PER_CROP,
+                             "mode": "trunk forward inside the training step (batch statistics)"},
+        "forward_roofline_eval": {"bound": "hbm", "fwd_ms": round(ev_ms, 4), "achieved": round(ev_gbs, 1),
+                                  "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ev_gbs / PEAK_HBM_GBS, 4),
+                                  "algorithmic_bytes_per_crop": FWD_BYTES_PER_CROP,
+                                  "crops_per_s": round(tr.B / (ev_ms * 1e-3), 1),
+                                  "mode": "PoseNetRGBDGeometric eval forward bs32 bf16 (running-stat BN folded into "
+                                          "the conv epilogues), hipGraph replay"},
     }
 
 
@@ -338,6 +348,26 @@ def inference_latency(dev, reps=50):
             graph = _time_fn(g.replay, reps)
         out[name] = {"eager_ms": round(eager * 1e3, 4), "graph_ms": round(graph * 1e3, 4)}
     return out
+
+
+def eval_forward_time(dev, B, reps=20):
+    """PoseNetRGBDGeometric eval forward (rotation head + pinhole translation) of one
+    bs-B batch in bf16, captured into a hipGraph; ms per replay."""
+    from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
+    torch.manual_seed(0)
+    m = PoseNetRGBDGeometric(pretrained=False).to(dev).set_compute_dtype(torch.bfloat16).eval()
+    b = synth_batch(B, dev, seed=1)
+    args = (b[0], None, b[1], b[2], b[3])
+    with torch.no_grad():
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            m(*args)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            m(*args)
+        return _time_fn(g.replay, reps) * 1e3
 
 
 def forward_time(tr, reps=20):

@@ -176,6 +176,13 @@ int pose6d_conv2d_fwd(int32_t dtype, const void *x, const void *wp, const float 
 int pose6d_conv_variant(int32_t dtype, int32_t pass, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout,
                         int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo);
 int pose6d_wgrad_variant(int32_t dtype, int32_t M, int32_t Cout, int32_t K, int32_t Cin);
+/* eval-mode forward with the BatchNorm folded into the store: out = act(T(conv(x) [+ bias]) * scale + shift
+ * [+ res | + res * res_scale + res_shift]), act = ReLU if relu -- pose6d_conv2d_fwd followed by
+ * pose6d_bn_act_fwd bit for bit, one launch, no raw-output round trip.  res: NHWC like out (or NULL). */
+int pose6d_conv2d_fwd_act(int32_t dtype, const void *x, const void *w, const float *bias, void *out, int32_t N,
+                          int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
+                          int32_t pad, int32_t Ho, int32_t Wo, const float *scale, const float *shift, const void *res,
+                          const float *res_scale, const float *res_shift, int32_t relu, void *stream);
 /* data gradient: dx [N][H][W][Cin] = conv_transpose(dy [N][Ho][Wo][Cout], wt) (+ dres if non-NULL).
  * dres may be dx itself (accumulate in place); a stride-2 1x1 conv then writes only the
  * pixels its taps reach (the other three parity classes are left as they are). */
@@ -259,6 +266,19 @@ int pose6d_bn_finalize(const float *partial, int32_t rows, int32_t C, int64_t co
                        const float *beta, float *running_mean, float *running_var, int64_t *num_batches,
                        float momentum, float eps, int32_t training, float *scale, float *shift, float *save_mean,
                        float *save_invstd, double *workspace, void *stream);
+/* Eval-mode fold of a table of BatchNorms in one launch: per entry and channel c,
+ * scale = gamma / sqrt(running_var + eps), shift = beta - running_mean * scale,
+ * save_mean = running_mean, save_invstd = 1 / sqrt(running_var + eps) -- pose6d_bn_finalize
+ * with training = 0, for all entries.  descs: device array of n pose6d_bn_fold_t
+ * (pose6d_bn_fold_desc_size() bytes each), max_c >= every entry's C. */
+typedef struct {
+  const float *gamma, *beta, *running_mean, *running_var;
+  float *scale, *shift, *save_mean, *save_invstd;
+  float eps;
+  int32_t C;
+} pose6d_bn_fold_t;
+int pose6d_bn_fold_desc_size(void);
+int pose6d_bn_eval_fold(const void *descs, int32_t n, int32_t max_c, void *stream);
 /* out = act(y * scale + shift [+ res | + res * res_scale + res_shift]); act = ReLU if relu */
 int pose6d_bn_act_fwd(int32_t dtype, const void *y, const float *scale, const float *shift, const void *res,
                       const float *res_scale, const float *res_shift, int32_t relu, void *out, int64_t M, int32_t C,

@@ -37,3 +37,22 @@ def test_b1_eval_forward_and_graph_replay(name):
         rot2, trans2 = _model_forward(name, m, cin)
         torch.cuda.synchronize()
     assert torch.equal(grot, rot2) and torch.equal(gtrans, trans2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("name", list(EXPECTED))
+def test_eval_bn_folded_into_conv_is_bit_identical(name, dtype, monkeypatch):
+    """Eval forward with BN + residual + ReLU applied in the conv epilogue
+    (pose6d_conv2d_fwd_act) equals the separate conv / bn_act launches bit for bit."""
+    torch.manual_seed(0)
+    m = _models()[name](pretrained=False).cuda().eval().set_compute_dtype(dtype)
+    g = torch.Generator().manual_seed(5)
+    cin = {k: v.cuda() for k, v in _inputs(2, 224, g).items()}
+    outs = []
+    for fold in ("0", "1"):
+        monkeypatch.setenv("POSE6D_EVAL_FUSE", fold)
+        with torch.no_grad():
+            rot, trans = _model_forward(name, m, cin)
+        torch.cuda.synchronize()
+        outs.append((rot.clone(), trans.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])

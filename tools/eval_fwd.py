@@ -1,0 +1,29 @@
+"""Eval-mode forward time at bs32 (bf16 and fp32), with and without the BN folded into the
+conv epilogues (POSE6D_EVAL_FUSE): usage python tools/eval_fwd.py"""
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "6d-pose-estimation_amd")]
+
+from bench import _time_fn, synth_batch  # noqa: E402
+from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda")
+    b = synth_batch(32, dev, seed=0)
+    args = (b[0], None, b[1], b[2], b[3])
+    for dt in (torch.bfloat16, torch.float32):
+        m = PoseNetRGBDGeometric(pretrained=False).to(dev).set_compute_dtype(dt).eval()
+        for fold in ("0", "1"):
+            os.environ["POSE6D_EVAL_FUSE"] = fold
+            with torch.no_grad():
+                t = _time_fn(lambda: m(*args), 20)
+            print(f"{dt} fold={fold}: {t * 1e3:.3f} ms/batch  {32 / t:.0f} crops/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
