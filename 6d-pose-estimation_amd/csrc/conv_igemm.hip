@@ -99,7 +99,9 @@ __device__ __forceinline__ int64_t out_row(const Geom& g, int cls, int m) {
 
 // Shared epilogue: + bias, BatchNorm partial statistics, LDS-staged 16-B stores
 // (+ residual).  Must be entered after a barrier that ends all LDS reads.
-template <typename T, int BM, int BN, bool BNF = false>
+// ACT: the eval BN-act store (Geom::act) compiled in (1) or out (0): the launchers
+// instantiate both, so the training kernels carry no trace of it
+template <typename T, int BM, int BN, bool BNF = false, int ACT = 0>
 __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const Geom& g,
                                               const float* __restrict__ bias, const T* __restrict__ res,
                                               T* __restrict__ out, float* __restrict__ stats, int m0, int n0,
@@ -208,7 +210,8 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], ch
   // iteration, so its channels' constants are loaded once
   static_assert(kThreads % CPR == 0, "store loop: fixed chunk column per thread");
   float asc[E], ash[E], arsc[E], arsh[E];
-  if (g.act) {
+  constexpr bool act = ACT == 1;
+  if (act) {
     const int c = n0 + (tid % CPR) * E;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -229,7 +232,7 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], ch
     uint4 v = *reinterpret_cast<const uint4*>(smem + lr * CROW + cc * 16);
     const int64_t om = out_row(g, cls, m);
     T* dst = out + om * g.Ncols + c;
-    if (g.act) {
+    if (act) {
       // pose6d_bn_act_fwd's arithmetic on the stored (T-rounded) conv output
       T a[E], b[E];
       __builtin_memcpy(a, &v, 16);
@@ -314,7 +317,7 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], ch
   }
 }
 
-template <typename T, int BM, int BN, int MODE>
+template <typename T, int BM, int BN, int MODE, bool ACT>
 __global__ __launch_bounds__(kThreads) void conv_igemm_kernel(const T* __restrict__ src, const T* __restrict__ wts,
                                                               const float* __restrict__ bias, const T* __restrict__ res,
                                                               T* __restrict__ out, float* __restrict__ stats, Geom g) {
@@ -492,7 +495,7 @@ __global__ __launch_bounds__(kThreads) void conv_igemm_kernel(const T* __restric
     __syncthreads();
   }
 
-  conv_epilogue<T, BM, BN>(acc, smem, g, bias, res, out, stats, m0, n0);
+  conv_epilogue<T, BM, BN, false, ACT ? 1 : 0>(acc, smem, g, bias, res, out, stats, m0, n0);
 }
 
 // ============================================================================
@@ -567,7 +570,7 @@ constexpr bool kPairedFrags = POSE6D_PAIRED_FRAGS;
 
 // one workgroup's work; `bid_in` = its index in this conv's sub-grid (the whole grid,
 // or the leading part of a fused backward launch), `smem` = the kernel's dynamic LDS
-template <int BM, int BN, int MODE, int S, bool BNF = false>
+template <int BM, int BN, int MODE, int S, bool BNF = false, bool ACT = false>
 __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16* __restrict__ src,
                                               const bf16* __restrict__ wts, const float* __restrict__ bias,
                                               const bf16* __restrict__ res, bf16* __restrict__ out,
@@ -795,17 +798,17 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
     wbuf = wbuf == S - 1 ? 0 : wbuf + 1;
   }
   asm volatile("s_barrier" ::: "memory");   // every wave done reading the ring before the epilogue reuses it
-  conv_epilogue<bf16, BM, BN, BNF>(acc, smem, g, bias, res, out, stats, m0, n0, cls, bn,
+  conv_epilogue<bf16, BM, BN, BNF, ACT ? 1 : 0>(acc, smem, g, bias, res, out, stats, m0, n0, cls, bn,
                                    MODE == kDgradS2 ? tm * 4 + cls : tm);
 }
 
-template <int BM, int BN, int MODE, int S>
+template <int BM, int BN, int MODE, int S, bool ACT>
 __global__ __launch_bounds__(kThreads) void conv_lds_kernel(const bf16* __restrict__ src, const bf16* __restrict__ wts,
                                                             const float* __restrict__ bias,
                                                             const bf16* __restrict__ res, bf16* __restrict__ out,
                                                             float* __restrict__ stats, Geom g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv_lds_body<BM, BN, MODE, S>(smem, blockIdx.x, src, wts, bias, res, out, stats, g);
+  conv_lds_body<BM, BN, MODE, S, false, ACT>(smem, blockIdx.x, src, wts, bias, res, out, stats, g);
 }
 
 // Fused backward of one conv: workgroups [0, nd) compute the data gradient,
@@ -862,8 +865,16 @@ int launch_fast(const Geom& g0, const void* src, const void* w, const float* bia
   const int lds = ring > epi ? ring : epi;
   if (MODE == kDgradS2) s2_single_class(g, res, out);
   const int grid = g.gm * g.gn * (MODE == kDgradS2 ? s2_classes(g) : 1);
-  conv_lds_kernel<BM, BN, MODE, S><<<grid, kThreads, lds, s>>>((const bf16*)src, (const bf16*)w, bias,
-                                                                (const bf16*)res, (bf16*)out, stats, g);
+  if constexpr (MODE == kGemm || MODE == kFwd) {
+    if (g.act) {   // eval BN-act epilogue (pose6d_conv2d_fwd_act)
+      conv_lds_kernel<BM, BN, MODE, S, true><<<grid, kThreads, lds, s>>>((const bf16*)src, (const bf16*)w, bias,
+                                                                         (const bf16*)res, (bf16*)out, stats, g);
+      P6_LAUNCH_CHECK();
+      return POSE6D_OK;
+    }
+  }
+  conv_lds_kernel<BM, BN, MODE, S, false><<<grid, kThreads, lds, s>>>((const bf16*)src, (const bf16*)w, bias,
+                                                                       (const bf16*)res, (bf16*)out, stats, g);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
@@ -911,7 +922,15 @@ int launch_t(const Geom& g0, const void* src, const void* w, const float* bias, 
   const int stage = 2 * (BM + BN) * 64;
   const int epi = BM * (BN * (int)sizeof(T) + 16);
   const int lds = stage > epi ? stage : epi;
-  conv_igemm_kernel<T, BM, BN, MODE><<<g.gm * g.gn, kThreads, lds, s>>>(
+  if constexpr (MODE != kDgrad) {
+    if (g.act) {   // eval BN-act epilogue (pose6d_conv2d_fwd_act)
+      conv_igemm_kernel<T, BM, BN, MODE, true><<<g.gm * g.gn, kThreads, lds, s>>>(
+          (const T*)src, (const T*)w, bias, (const T*)res, (T*)out, stats, g);
+      P6_LAUNCH_CHECK();
+      return POSE6D_OK;
+    }
+  }
+  conv_igemm_kernel<T, BM, BN, MODE, false><<<g.gm * g.gn, kThreads, lds, s>>>(
       (const T*)src, (const T*)w, bias, (const T*)res, (T*)out, stats, g);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;

@@ -18,8 +18,8 @@ def _sym(v, T):
     bm, bn = TILES[v & 15]
     mode = (v >> 4) & 15
     if (v >> 8) & 1:
-        return f"conv_lds_kernel<{bm}, {bn}, {mode}, {v >> 12}>"
-    return f"conv_igemm_kernel<{T}, {bm}, {bn}, {mode}>"
+        return f"conv_lds_kernel<{bm}, {bn}, {mode}, {v >> 12}, false>"
+    return f"conv_igemm_kernel<{T}, {bm}, {bn}, {mode}, false>"
 
 
 def conv_launches(eng, fused=True):
