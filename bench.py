@@ -103,12 +103,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("POSE6D_BENCH_SHARE_GPU"):
+        local %= torch.cuda.device_count()   # rehearsal of the N > 1 path on a one-GPU box only
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if os.environ.get("POSE6D_BENCH_SHARE_GPU"):
+            dist.init_process_group("gloo")   # RCCL refuses two ranks on one device
+        else:
+            dist.init_process_group("nccl", device_id=dev)
         pg = dist.group.WORLD
 
     from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
