@@ -166,7 +166,30 @@ __global__ __launch_bounds__(kThreads) void linear_wgrad_kernel(const float* __r
   float acc[4][4] = {};
   float bs[4] = {0.f, 0.f, 0.f, 0.f};
   const bool vec = xvec && k0 + 3 < K;
-  for (int b = 0; b < Bn; ++b) {
+  // batch rows 8 at a time with every load issued first (one memory round trip per
+  // 8 rows instead of per row); same per-element fma order as the row loop below
+  constexpr int RB = 8;
+  int b = 0;
+  if (vec)
+    for (; b + RB <= Bn; b += RB) {
+      f32x4 xr[RB];
+      float dr[RB][4];
+#pragma unroll
+      for (int u = 0; u < RB; ++u) {
+        xr[u] = *reinterpret_cast<const f32x4*>(x + (b + u) * ldx + k0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dr[u][i] = nb + i < N ? dy[(b + u) * ldy + nb + i] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < RB; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          bs[i] += dr[u][i];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(dr[u][i], xr[u][j], acc[i][j]);
+        }
+    }
+  for (; b < Bn; ++b) {
     float xv[4];
     if (vec) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(x + b * ldx + k0);
