@@ -96,3 +96,35 @@ def test_trainer_checkpoint_interop():
         o = tr3.arena.offsets[tr3.arena._index_of(p)]
         assert torch.equal(p.detach(), q.detach())
         assert torch.equal(tr3.m[o:o + p.numel()], opt.state[q]["exp_avg"].reshape(-1))
+
+
+def test_trainer_clip_and_adamw_match_torch():
+    """The trainer's clip-norm + AdamW launches (pose6d_sumsq_partial_step +
+    pose6d_adamw_step) against torch.nn.utils.clip_grad_norm_(params, 1.0) +
+    torch.optim.AdamW (train_rgbd_geometric.py:111-112) on a gradient whose norm
+    is well above 1, so the clip is active."""
+    from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
+    from pose6d.train import RGBDGeometricTrainer
+    warnings.simplefilter("ignore")
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    model = PoseNetRGBDGeometric(pretrained=False).to(dev)
+    tr = RGBDGeometricTrainer(model, 4, dtype=torch.bfloat16)
+    m2 = PoseNetRGBDGeometric(pretrained=False).to(dev)
+    m2.load_state_dict(model.state_dict())
+    params2 = list(m2.parameters())
+    opt = torch.optim.AdamW(params2, lr=1e-4, weight_decay=1e-4)
+    gen = torch.Generator(device=dev).manual_seed(3)
+    for _ in range(3):
+        g = torch.randn(tr.arena.numel, device=dev, generator=gen) * 0.05   # total norm ~ 250
+        for p, q in zip(model.parameters(), params2):
+            o = tr.arena.offsets[tr.arena._index_of(p)]
+            q.grad = g[o:o + p.numel()].view_as(q).clone()
+        norm_ref = torch.nn.utils.clip_grad_norm_(params2, 1.0)
+        opt.step()
+        tr.arena.grad.copy_(g)
+        tr._optimizer()
+        torch.cuda.synchronize()
+        torch.testing.assert_close(tr.norm[0], norm_ref.float(), rtol=1e-5, atol=0)
+    for (k, p), q in zip(model.named_parameters(), params2):
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-6, atol=1e-7, msg=k)
