@@ -3,9 +3,9 @@
 //
 // One launch covers the whole batch (no per-sample host loop, no .item() syncs):
 //   add_points_kernel  grid (ceil(maxN/512), B): each block owns 512 predicted
-//                      points of one sample (2 per lane, one packed-fp32 pair: at 4 per
-//                      lane the 2000-point meshes left 2 waves per SIMD and the loop
-//                      latency-bound), streams that sample's
+//                      points of one sample (2 per lane: at 4 per lane the 2000-point
+//                      meshes left 2 waves per SIMD and the loop latency-bound; at 1,
+//                      every gt tile is transformed and read for half the work), streams that sample's
 //                      transformed ground-truth mesh through LDS in 2048-point tiles
 //                      (broadcast ds_read_b128, no bank conflicts) and keeps a running
 //                      nearest-point minimum per predicted point in registers.
@@ -27,7 +27,6 @@ constexpr int kPtsPerBlock = kThreads * kPPT;
 constexpr int kTile = 2048;                   // gt points per LDS tile (32 KiB)
 
 struct Mat3 { float r[9]; };
-typedef float f2 __attribute__((ext_vector_type(2)));
 
 // add_loss.py:203-215, every op rounded separately
 __device__ __forceinline__ Mat3 quat_to_mat(const float* q) {
@@ -109,14 +108,6 @@ __global__ __launch_bounds__(kThreads) void add_points_kernel(
     }
   }
 
-  static_assert(kPPT % 2 == 0, "predicted points go in packed pairs");
-  f2 qx2[kPPT / 2], qy2[kPPT / 2], qz2[kPPT / 2];
-#pragma unroll
-  for (int p = 0; p < kPPT / 2; ++p) {
-    qx2[p] = f2{qx[2 * p], qx[2 * p + 1]};
-    qy2[p] = f2{qy[2 * p], qy[2 * p + 1]};
-    qz2[p] = f2{qz[2 * p], qz[2 * p + 1]};
-  }
   for (int j0 = 0; j0 < n; j0 += kTile) {
     const int jn = min(kTile, n - j0);
     __syncthreads();
@@ -124,20 +115,12 @@ __global__ __launch_bounds__(kThreads) void add_points_kernel(
     __syncthreads();
     for (int jj = 0; jj < jn; ++jj) {
       const float4 g = gs[jj];
-      // two predicted points per packed-fp32 instruction (v_pk_add / v_pk_mul /
-      // v_pk_fma: the same IEEE rounding per element as sqdist's scalar ops)
 #pragma unroll
-      for (int p = 0; p < kPPT / 2; ++p) {
-        const f2 dx = qx2[p] - f2{g.x, g.x}, dy = qy2[p] - f2{g.y, g.y}, dz = qz2[p] - f2{g.z, g.z};
-        const f2 s2 = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int i = 2 * p + e;
-          const float s = s2[e];
-          if (s < best[i]) {
-            if (sqrtf(s) != sqrtf(best[i])) bi[i] = j0 + jj;
-            best[i] = s;
-          }
+      for (int i = 0; i < kPPT; ++i) {
+        const float s = sqdist(qx[i], qy[i], qz[i], g);
+        if (s < best[i]) {
+          if (sqrtf(s) != sqrtf(best[i])) bi[i] = j0 + jj;
+          best[i] = s;
         }
       }
     }
