@@ -98,6 +98,7 @@ def test_trainer_checkpoint_interop():
         assert torch.equal(tr3.m[o:o + p.numel()], opt.state[q]["exp_avg"].reshape(-1))
 
 
+@pytest.mark.gpu
 def test_trainer_clip_and_adamw_match_torch():
     """The trainer's clip-norm + AdamW launches (pose6d_sumsq_partial_step +
     pose6d_adamw_step) against torch.nn.utils.clip_grad_norm_(params, 1.0) +
