@@ -77,3 +77,56 @@ def synthetic_meshes(n_points=2000, seed=0, n_obj=13):
     pts = {oid: (rng.standard_normal((n_points, 3)) * 0.04).astype(np.float32) for oid in LINEMOD_OBJ_IDS[:n_obj]}
     diam = {oid: 0.1 + 0.1 * i / 12.0 for i, oid in enumerate(LINEMOD_OBJ_IDS[:n_obj])}
     return pts, diam
+
+
+def write_linemod_tree(root, n_frames=100, H=120, W=160, seed=0):
+    """A LineMOD_preprocessed/data-shaped tree (folder/{rgb,depth}/NNNN.png,
+    gt.yml, info.yml) exercising every branch of the reference index
+    (data/dataset_rgbd.py:31-82): a non-numeric folder, a folder without
+    info.yml, one without depth/ (RGB keeps it, RGB-D skips it), frames missing
+    from gt.yml or info.yml, annotations of other objects on a frame, a
+    non-PNG file among the frames and a missing depth PNG (read as zeros).
+    Returns {folder: {frame_id: (rgb, depth or None)}} of what was written."""
+    import yaml
+    from PIL import Image
+    from scipy.spatial.transform import Rotation
+    rng = np.random.default_rng(seed)
+    written = {}
+    os.makedirs(os.path.join(root, "notes"), exist_ok=True)
+    for folder in ("01", "03", "04", "06"):
+        base = os.path.join(root, folder)
+        os.makedirs(os.path.join(base, "rgb"), exist_ok=True)
+        if folder != "04":
+            os.makedirs(os.path.join(base, "depth"), exist_ok=True)
+        gts, infos, frames = {}, {}, {}
+        for f in range(n_frames):
+            rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+            Image.fromarray(rgb).save(os.path.join(base, "rgb", f"{f:04d}.png"))
+            depth = None
+            if folder != "04" and f != 18:
+                depth = rng.integers(300, 1600, (H, W)).astype(np.uint16)
+                depth[rng.random((H, W)) < 0.05] = 0
+                Image.fromarray(depth).save(os.path.join(base, "depth", f"{f:04d}.png"))
+            frames[f] = (rgb, depth)
+            w, h = (int(v) for v in rng.integers(20, 70, 2))
+            x, y = int(rng.integers(-10, W - w + 10)), int(rng.integers(-10, H - h + 10))
+            R = Rotation.from_quat(rng.standard_normal(4)).as_matrix()
+            anno = {"cam_R_m2c": [float(v) for v in R.reshape(-1)],
+                    "cam_t_m2c": [float(v) for v in rng.normal((0, 0, 800), 80, 3)],
+                    "obj_bb": [x, y, w, h], "obj_id": int(folder)}
+            other = dict(anno, obj_id=int(folder) % 15 + 1, obj_bb=[1, 2, 30, 30])
+            if f != 28:
+                gts[f] = [other, anno] if f % 7 == 0 else [anno]
+            if f != 38:
+                fx = float(rng.uniform(500, 600))
+                infos[f] = {"cam_K": [fx, 0.0, W / 2 + 3.5, 0.0, fx + 1.0, H / 2 - 2.25, 0.0, 0.0, 1.0],
+                            "depth_scale": 1.0}
+        with open(os.path.join(base, "rgb", "thumbs.db"), "w") as fh:
+            fh.write("x")
+        with open(os.path.join(base, "gt.yml"), "w") as fh:
+            yaml.safe_dump(gts, fh)
+        if folder != "03":
+            with open(os.path.join(base, "info.yml"), "w") as fh:
+                yaml.safe_dump(infos, fh)
+        written[folder] = frames
+    return written
