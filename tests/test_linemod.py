@@ -191,3 +191,31 @@ def test_evaluate_model_vs_oracle_add(tree, tmp_path):
             ref["acc"].append(m["add_01d_acc"])
     np.testing.assert_allclose([got["ADD (mm)"], got["ADD-S (mm)"], got["ADD-0.1d (%)"]],
                                [np.mean(ref["add"]), np.mean(ref["adds"]), np.mean(ref["acc"])], rtol=1e-6)
+
+
+@pytest.mark.gpu
+def test_compare_models_cli_on_checkpoints(tree, tmp_path):
+    """tools/compare_models.py end to end: reference-format checkpoints
+    ({'model_state_dict': ...}, torch.save) of two models, cat-only filter."""
+    import importlib.util
+    from models.pose_net_rgb_geometric import PoseNetRGBGeometric
+    from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
+    from tests.synth import write_mesh_dir
+    root, _ = tree
+    write_mesh_dir(str(tmp_path), n_vertices=300, seed=3)
+    torch.manual_seed(0)
+    args = ["--data-root", root, "--model-dir", str(tmp_path), "--objects", "06", "--batch-size", "5"]
+    for name, cls in (("RGB-Geometric", PoseNetRGBGeometric), ("RGBD-Geometric", PoseNetRGBDGeometric)):
+        p = str(tmp_path / f"{name}.pth")
+        torch.save({"epoch": 1, "model_state_dict": cls(pretrained=False).state_dict()}, p)
+        args += ["--weights", f"{name}={p}"]
+    args += ["--weights", f"RGB={tmp_path / 'absent.pth'}"]
+    spec = importlib.util.spec_from_file_location(
+        "compare_models", os.path.join(os.path.dirname(os.path.dirname(__file__)), "tools", "compare_models.py"))
+    cm = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(cm)
+    res = cm.main(args)
+    assert sorted(res) == ["RGB-Geometric", "RGBD-Geometric"]
+    for m in res.values():
+        assert all(np.isfinite(v) for v in m.values())
+        assert 0.0 <= m["ADD-0.1d (%)"] <= 100.0
