@@ -14,7 +14,11 @@ MI355X design:
   * data parallel: one process per GPU, batch shards, gradient all-reduce over
     RCCL (torch.distributed 'nccl'); bucketed all-reduces are issued on a comm
     stream as soon as each bucket's gradients exist, overlapping the rest of the
-    backward (replay is split at bucket boundaries for that).
+    backward.  For that the captured step is cut into segments at the launches
+    that complete a bucket: replay = segment, all-reduce of the buckets it
+    finished (comm stream, event-ordered), next segment, ..., then the
+    optimizer graph once every all-reduce has landed (a handful of host calls
+    per step instead of ~300 eager launches).
 """
 import math
 
@@ -173,8 +177,9 @@ class RGBDGeometricTrainer:
 
     # ------------------------------------------------------------- graphs
     def capture(self, data, warmup=2):
-        """Capture the step (world == 1: one graph; world > 1: forward+head graph,
-        eager bucketed backward, optimizer graph)."""
+        """Capture the step.  world == 1: one graph.  world > 1: the forward +
+        backward as graph segments cut where a gradient bucket completes, and the
+        optimizer as a graph of its own (the all-reduces run between replays)."""
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -192,26 +197,84 @@ class RGBDGeometricTrainer:
                 self._optimizer()
             self.graphs = [g]
         else:
-            g1 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1):
-                self.trunk.pack_weights(force=True)
-                self._forward_loss(*data)
-                self._dfeat = self._head_backward()
-            g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2):
-                self._optimizer()
-            self.graphs = [g1, g2]
+            self.graphs = self._capture_segments(data)
         torch.cuda.synchronize()
+
+    def _capture_segments(self, data):
+        """[(graph, buckets it completes)] for forward + backward, then the optimizer
+        graph.  Segment boundaries are the launches after which on_conv_done makes
+        a bucket ready: exactly where the eager path issues that bucket."""
+        pool = torch.cuda.graph_pool_handle()
+        ends = [e for _, e in self.bucket_ends]
+        segs = []
+        st = {"g": None, "next": 0}
+        cs = torch.cuda.Stream(device=self.dev)
+        cs.wait_stream(torch.cuda.current_stream())
+
+        def begin():
+            st["g"] = torch.cuda.CUDAGraph()
+            st["g"].capture_begin(pool=pool)
+
+        def cut(upto):
+            # the last bucket (ending at the arena end) always goes out after the
+            # final segment, which therefore never comes out empty
+            first = st["next"]
+            while st["next"] < len(ends) - 1 and ends[st["next"]] <= upto:
+                st["next"] += 1
+            if st["next"] > first:
+                st["g"].capture_end()
+                segs.append((st["g"], (first, st["next"])))
+                begin()
+
+        def on_conv(op):
+            last = op.conv.bias if op.conv.bias is not None else op.conv.weight
+            cut(self.arena.end_offset(last))
+
+        with torch.cuda.stream(cs):
+            begin()
+            self.trunk.pack_weights(force=True)
+            self._forward_loss(*data)
+            dfeat = self._head_backward()
+            self.trunk.backward(dfeat, self.arena.grad_of, on_conv_done=on_conv)
+            st["g"].capture_end()
+            segs.append((st["g"], (st["next"], len(ends))))
+            opt = torch.cuda.CUDAGraph()
+            opt.capture_begin(pool=pool)
+            self._optimizer()
+            opt.capture_end()
+        torch.cuda.current_stream().wait_stream(cs)
+        self._red = BucketReducer(self.arena.grad, self.bucket_ends, self.pg, self._comm_stream())
+        return segs + [(opt, None)]
 
     def step(self, data=None):
         if self.graphs is None:
             return self.step_eager(data)
         if self.world == 1:
             self.graphs[0].replay()
-        else:
-            self.graphs[0].replay()
-            self._backward_ddp(self._dfeat)
-            self.graphs[1].replay()
+            return
+        red = self._red
+        red.reset()
+        ends = red.ends
+        for g, buckets in self.graphs[:-1]:
+            g.replay()
+            lo, hi = buckets
+            if hi > lo:
+                red.ready(ends[hi - 1])
+        red.finish()
+        self.graphs[-1][0].replay()
+
+    def snapshot(self):
+        """Device copies of everything a step changes (parameters, AdamW moments and
+        step, dropout seed, BN buffers) -- restore() rewinds to it in place, so a
+        captured graph keeps running on the same storage."""
+        bufs = [b for n, b in self.model.named_buffers() if "running" in n or "num_batches" in n]
+        return [t.clone() for t in (self.arena.flat, self.m, self.v, self.hp, self.seed, *bufs)]
+
+    def restore(self, snap):
+        bufs = [b for n, b in self.model.named_buffers() if "running" in n or "num_batches" in n]
+        with torch.no_grad():
+            for dst, src in zip((self.arena.flat, self.m, self.v, self.hp, self.seed, *bufs), snap):
+                dst.copy_(src)
 
     def set_lr(self, lr):
         self.hp[0].fill_(lr)

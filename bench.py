@@ -53,13 +53,40 @@ def synth_batch(B, dev, seed):
     return [t.to(dev).contiguous() for t in (rgb, depth_raw, bbox, K, gt_rot, gt_trans)]
 
 
-def cpu_baseline(batch=32, steps=2, threads=None):
+def host_cpu():
+    """(threads the CPU baselines use, CPU model, os.cpu_count()).  The GPU box's
+    os.cpu_count() reports the whole machine while a job gets a share of it (the
+    affinity mask / cgroup quota): the baselines use that share, not oversubscribed."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return n, model, os.cpu_count()
+
+
+def _cpu_meta(threads, model, total, kind, sample, value, unit):
+    return {"value": value, "unit": unit, "cores": threads, "kind": kind, "sample": sample, "cpu_model": model,
+            "os_cpu_count": total}
+
+
+def cpu_baseline(batch=32, steps=2):
     """The oracle (torch-CPU fp32 restatement, shown equal to the reference on the
     golden fixtures) doing the same training step on the host cores."""
     from oracle import pose_loss as OP
     from oracle import resnet as OR
     from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
-    threads = threads or min(16, os.cpu_count() or 1)
+    threads, model, total = host_cpu()
     torch.set_num_threads(threads)
     torch.manual_seed(0)
     m = PoseNetRGBDGeometric(pretrained=False)
@@ -80,9 +107,51 @@ def cpu_baseline(batch=32, steps=2, threads=None):
     for _ in range(steps):
         one()
     dt = time.perf_counter() - t0
-    return {"value": round(batch * steps / dt, 3), "unit": "crops/s", "cores": threads, "kind": "port",
-            "sample": f"oracle torch-CPU fp32 train step (fwd+loss+bwd+clip+AdamW), batch {batch}, "
-                      f"{steps} timed steps after 1 warmup, {threads} threads"}
+    return _cpu_meta(threads, model, total, "port",
+                     f"oracle torch-CPU fp32 train step (fwd+loss+bwd+clip+AdamW), batch {batch}, {steps} timed steps "
+                     f"after 1 warmup, {threads} threads", round(batch * steps / dt, 3), "crops/s")
+
+
+def cpu_baseline_c1(batch=4, iters=5):
+    """BASELINE configs[0] (C1): PoseNetRGB forward + PoseLoss at batch 4 on the CPU
+    (oracle torch-CPU fp32 restatement; train-mode BN, no_grad, as BASELINE.md §3)."""
+    from oracle import pose_loss as OP
+    from oracle import resnet as OR
+    from models.pose_net_rgb import PoseNetRGB
+    threads, model, total = host_cpu()
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    P = {k: v.clone() for k, v in PoseNetRGB(pretrained=False).state_dict().items()}
+    rgb, _, _, _, gr, gt = synth_batch(batch, "cpu", 5)
+    with torch.no_grad():
+        def one():
+            rot, trans = OR.forward_rgb(P, rgb, True)
+            OP.pose_loss(rot, trans, gr, gt, 1.0, 10.0)
+        one()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            one()
+        dt = time.perf_counter() - t0
+    return _cpu_meta(threads, model, total, "port", f"oracle torch-CPU fp32 PoseNetRGB forward + PoseLoss, batch {batch}, "
+                     f"{iters} timed iterations after 1 warmup", round(batch * iters / dt, 2), "crops/s")
+
+
+def cpu_baseline_add(pts, diam, args, n=32):
+    """BASELINE configs[3] (C4) on the CPU: the reference's eval_metrics loop
+    (torch-CPU per-sample ops, oracle.add_loss.eval_metrics_torch) over the first
+    `n` samples of the same synthetic bs256 x 2000-point batch."""
+    from oracle import add_loss as OA
+    threads, model, total = host_cpu()
+    torch.set_num_threads(threads)
+    P = {k: torch.from_numpy(v) for k, v in pts.items()}
+    cargs = [a[:n].cpu() for a in args]
+    OA.eval_metrics_torch(P, diam, *[a[:2] for a in cargs])
+    t0 = time.perf_counter()
+    OA.eval_metrics_torch(P, diam, *cargs)
+    dt = time.perf_counter() - t0
+    return _cpu_meta(threads, model, total, "port", f"reference eval_metrics loop restated in torch-CPU ops "
+                     f"(oracle.add_loss.eval_metrics_torch), first {n} of the bs256 x 2000-point samples",
+                     round(n / dt, 2), "samples/s")
 
 
 def main():
@@ -166,13 +235,20 @@ def main():
     if rank == 0 and not args.no_kernel_profile:
         result.update(kernel_profile(tr, ms))
     if rank == 0 and not args.no_side:
-        result["side_configs"] = {"configs[1]": rgb_fp32_forward(dev), "configs[3]": add_eval_throughput(dev),
+        result["side_configs"] = {"configs[1]": rgb_fp32_forward(dev),
+                                  "configs[3]": add_eval_throughput(dev, cpu=not args.no_cpu_baseline),
                                   "frame_crops": crop_throughput(dev), "inference_b1": inference_latency(dev)}
     if rank == 0 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline()
         except Exception as e:  # noqa: BLE001 - report, do not fail the bench line
             result["cpu_baseline"] = {"value": None, "error": repr(e)}
+        try:
+            result.setdefault("side_configs", {})["configs[0]"] = {
+                "workload": "PoseNetRGB forward + PoseLoss, batch 4, 224^2, CPU (BASELINE configs[0])",
+                "cpu_baseline": cpu_baseline_c1()}
+        except Exception as e:  # noqa: BLE001
+            result.setdefault("side_configs", {})["configs[0]"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -266,7 +342,7 @@ def rgb_fp32_forward(dev, B=32, reps=10):
                              "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_bytes_per_crop": FWD_BYTES_PER_CROP_F32}}
 
 
-def add_eval_throughput(dev, B=256, N=2000, reps=10):
+def add_eval_throughput(dev, B=256, N=2000, reps=10, cpu=True):
     """BASELINE configs[3]: ADD/ADD-S eval of bs256 x 2000 mesh points x 13 objects
     (SURVEY.md §8d synthetic meshes / perturbed poses) through ADDLoss.per_sample
     (one pose6d_add_eval call) -> samples/s, ADD-S pairs/s, fraction of the fp32
@@ -285,7 +361,13 @@ def add_eval_throughput(dev, B=256, N=2000, reps=10):
     t = _time_fn(lambda: crit.per_sample(*args), reps)
     pairs = float(sum(pts[int(i)].shape[0] ** 2 for i in ids))
     m = crit.eval_metrics(*args)
-    return {"workload": f"ADDLoss eval bs{B} x {N} pts x {len(pts)} objects (ADD, ADD-S, 0.1d)",
+    extra = {}
+    if cpu:
+        try:
+            extra["cpu_baseline"] = cpu_baseline_add(pts, diam, args)
+        except Exception as e:  # noqa: BLE001
+            extra["cpu_baseline"] = {"value": None, "error": repr(e)}
+    return {**extra, "workload": f"ADDLoss eval bs{B} x {N} pts x {len(pts)} objects (ADD, ADD-S, 0.1d)",
             "value": round(B / t, 1), "unit": "samples/s", "ms_per_batch": round(t * 1e3, 4), "dtype": "f32",
             "pairs_per_s": round(pairs / t, 1), "add_01d_acc": round(float(m["add_01d_acc"]), 3),
             "valu_roofline": {"achieved": round(pairs * ADD_FLOPS_PER_PAIR / t / 1e12, 2), "peak": PEAK_F32_VALU_TFLOPS,

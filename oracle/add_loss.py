@@ -216,3 +216,36 @@ def load_models(model_dir, num_points=500):
             pts = pts[np.random.choice(pts.shape[0], num_points, replace=False)]
         points[oid] = pts.astype(np.float32)
     return points, diameters
+
+
+def eval_metrics_torch(points, diameters, pred_r, pred_t, gt_r, gt_t, obj_ids):
+    """add_loss.py:156-201 as the reference runs it: torch-CPU ops per sample
+    (mm + t, norm, the (N, N, 3) pairwise tensor, min over the gt points) --
+    the CPU baseline of BASELINE configs[3] (bench.py), on the host's threads.
+    points: {oid: (N, 3) float32 torch tensor}; the rest torch tensors."""
+    import torch
+
+    def q2m(q):                                              # add_loss.py:203-215
+        x, y, z, w = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+        return torch.stack([
+            torch.stack([1 - 2 * y * y - 2 * z * z, 2 * x * y - 2 * w * z, 2 * x * z + 2 * w * y], 1),
+            torch.stack([2 * x * y + 2 * w * z, 1 - 2 * x * x - 2 * z * z, 2 * y * z - 2 * w * x], 1),
+            torch.stack([2 * x * z - 2 * w * y, 2 * y * z + 2 * w * x, 1 - 2 * x * x - 2 * y * y], 1)], 1)
+
+    pR, gR = q2m(pred_r), q2m(gt_r)
+    adds_, addss, corr = [], [], []
+    for i in range(pred_r.shape[0]):
+        oid = int(obj_ids[i].item())
+        if oid not in points:
+            continue
+        P = points[oid]
+        G = torch.mm(P, gR[i].T) + gt_t[i]
+        Q = torch.mm(P, pR[i].T) + pred_t[i]
+        add = torch.norm(Q - G, dim=1, p=2).mean().item()
+        adds = torch.norm(Q.unsqueeze(1) - G.unsqueeze(0), dim=2).min(dim=1)[0].mean().item()
+        d = adds if oid in SYMMETRIC_OBJECT_IDS else add
+        adds_.append(add)
+        addss.append(adds)
+        corr.append(float(d < 0.1 * diameters.get(oid, 0.1)))
+    return {"add_mean": np.mean(adds_) * 1000 if adds_ else 0, "add_s_mean": np.mean(addss) * 1000 if addss else 0,
+            "add_01d_acc": np.mean(corr) * 100 if corr else 0}

@@ -1,8 +1,12 @@
 """Worker of tests/test_ddp_gpu.py (launched by torch.distributed.run, 2 ranks on
-ONE GPU over gloo: RCCL needs a GPU per rank).  Both ranks train one step on the
-same batch through the bucketed all-reduce path (RGBDGeometricTrainer with a
-process group); the averaged gradient then equals each rank's own, so the
-updated parameters must equal a single-process step bit for bit."""
+ONE GPU over gloo: RCCL needs a GPU per rank).  Each rank trains one step on its
+OWN batch (seed 77 + rank) through the bucketed all-reduce path
+(RGBDGeometricTrainer with a process group), eagerly and replayed from the
+segmented graphs.  Rank 0 also builds the expected update in one process: the
+gradients of the two batches from two 1-process trainers, averaged, fed to the
+same clip-norm + AdamW step.  With two ranks the all-reduce sum is exact
+(a + b == b + a), so the parameters must agree bit for bit; each rank's BatchNorm
+running statistics must equal a 1-process step on its own batch (local BN)."""
 import os
 import sys
 
@@ -16,34 +20,71 @@ import torch.distributed as dist  # noqa: E402
 def main():
     out = sys.argv[1]
     dist.init_process_group("gloo")
-    rank = dist.get_rank()
+    rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     from bench import synth_batch
     from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
     from pose6d.train import RGBDGeometricTrainer
     B = 4
-    data = synth_batch(B, dev, seed=77)
+    batches = [synth_batch(B, dev, seed=77 + r) for r in range(world)]
 
-    def run(pg, bucket_mb):
+    def trainer(pg, bucket_mb=2.0):
         torch.manual_seed(0)
         model = PoseNetRGBDGeometric(pretrained=False).to(dev)
         for m in model.modules():
             if isinstance(m, torch.nn.Dropout):
                 m.eval()
-        tr = RGBDGeometricTrainer(model, B, dtype=torch.bfloat16, process_group=pg, bucket_mb=bucket_mb)
-        tr.step_eager(data)
-        torch.cuda.synchronize()
-        return tr.arena.flat.clone(), tr
+        return RGBDGeometricTrainer(model, B, dtype=torch.bfloat16, process_group=pg, bucket_mb=bucket_mb)
 
-    flat_ddp, tr = run(dist.group.WORLD, 2.0)    # small buckets: many all-reduces overlap backward
-    n_buckets = len(tr.bucket_ends)
-    if rank == 0:
-        flat_one, _ = run(None, 2.0)
-        same = bool(torch.equal(flat_ddp, flat_one))
-        diff = float((flat_ddp - flat_one).abs().max())
-        with open(out, "w") as f:
-            f.write(f"{int(same)} {diff} {n_buckets}\n")
+    def buffers(tr):
+        return torch.cat([v.float().flatten() for k, v in tr.model.state_dict().items() if "running" in k])
+
+    # eager bucketed step (small buckets: many all-reduces overlap backward)
+    tr = trainer(dist.group.WORLD)
+    tr.step_eager(batches[rank])
+    torch.cuda.synchronize()
+    flat_eager, n_buckets, run_eager = tr.arena.flat.clone(), len(tr.bucket_ends), buffers(tr)
+    # graph-segmented bucketed step: capture() runs 2 eager warm-up steps; re-seed the
+    # parameters/moments/buffers afterwards so the replayed step starts from the same state
+    trg = trainer(dist.group.WORLD)
+    snap = trg.snapshot()
+    trg.capture(batches[rank])
+    trg.restore(snap)
+    trg.step()
+    torch.cuda.synchronize()
+    flat_graph, run_graph, n_segs = trg.arena.flat.clone(), buffers(trg), len(trg.graphs) - 1
+
+    # every rank holds the same parameters
+    mine = flat_eager.cpu()
+    others = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(others, mine)
+    ranks_agree = all(torch.equal(o, mine) for o in others)
+
+    # 1-process reference: own-batch step (BN running stats) + mean-gradient update
+    ref = trainer(None)
+    ref.step_eager(batches[rank])
+    torch.cuda.synchronize()
+    run_ref = buffers(ref)
+    grads = []
+    for r in range(world):
+        t = trainer(None)
+        t.step_eager(batches[r])
+        torch.cuda.synchronize()
+        grads.append(t.arena.grad.clone())
+    t = trainer(None)
+    with torch.no_grad():
+        t.arena.grad.copy_(grads[0] + grads[1])
+        t.arena.grad.mul_(1.0 / world)
+    t._optimizer()
+    torch.cuda.synchronize()
+    flat_ref = t.arena.flat
+    res = [int(torch.equal(flat_eager, flat_ref)), float((flat_eager - flat_ref).abs().max()),
+           int(torch.equal(flat_graph, flat_eager)), int(torch.equal(run_eager, run_ref)),
+           int(torch.equal(run_graph, run_ref)), int(ranks_agree), n_buckets, n_segs,
+           int(not torch.equal(grads[0], grads[1]))]
+    with open(f"{out}.{rank}", "w") as f:
+        f.write(" ".join(str(x) for x in res) + "\n")
     dist.barrier()
     dist.destroy_process_group()
 

@@ -130,3 +130,16 @@ def write_linemod_tree(root, n_frames=100, H=120, W=160, seed=0):
                 yaml.safe_dump(infos, fh)
         written[folder] = frames
     return written
+
+
+def xattn_weights(D, seed):
+    """CrossModalAttention parameters from a seeded CPU generator (q, k, v, out
+    projections: N(0, 1/D) weights, N(0, 0.01) biases), as the model_parts fixture
+    (tools/gen_goldens.py) was made with; the fixture stores their checksums."""
+    import torch
+    g = torch.Generator().manual_seed(seed)
+    sd = {}
+    for n in ("q_proj", "k_proj", "v_proj", "out_proj"):
+        sd[n + ".weight"] = torch.randn(D, D, generator=g) * D ** -0.5
+        sd[n + ".bias"] = torch.randn(D, generator=g) * 0.1
+    return sd

@@ -8,15 +8,22 @@ inputs.  Nothing from the reference is copied: the fixtures are inputs + outputs
 
     python tools/gen_goldens.py            # rewrites tests/golden/*.npz
 
-The reference's `models/pose_net_*.py` need torchvision, which is absent from this
-image; no stand-in is written for it, so model-forward parity is anchored on the
-build's CPU restatement (oracle/resnet.py) -- see DESIGN.md "Oracle".
+The reference's `models/pose_net_*.py` import torchvision at module level, which is
+absent from this image.  Their torchvision-free parts -- `CrossModalAttention`
+(pose_net_rgbd.py:8-35) and both `_compute_pinhole_translation` methods
+(pose_net_rgbd_geometric.py:56-85, pose_net_rgb_geometric.py:93-109) -- are run
+by importing those files against a `torchvision` placeholder whose every
+attribute access RAISES: the module-level import succeeds, and no third-party
+arithmetic can enter a fixture (nothing here constructs a model, so nothing asks
+for `models.resnet50`).  The ResNet50 trunk stays parity-unpinned (DESIGN.md
+"Oracle").
 """
 import importlib.util
 import json
 import os
 import sys
 import tempfile
+import types
 
 import numpy as np
 import torch
@@ -24,7 +31,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 sys.path.insert(0, REPO)
-from tests.synth import write_mesh_dir, LINEMOD_OBJ_IDS, make_poses, grid_mesh  # noqa: E402
+from tests.synth import write_mesh_dir, LINEMOD_OBJ_IDS, make_poses, grid_mesh, xattn_weights  # noqa: E402
 
 REF = os.environ.get("POSE6D_REFERENCE", "/root/reference")
 OUT = os.path.join(REPO, "tests", "golden")
@@ -191,6 +198,103 @@ def gen_add(ref_al):
     np.savez_compressed(os.path.join(OUT, "add_loss.npz"), **out)
 
 
+class _Refuse(types.ModuleType):
+    """torchvision placeholder: importable, unusable."""
+
+    def __getattr__(self, name):
+        if name.startswith("__"):
+            raise AttributeError(name)
+        raise RuntimeError(f"torchvision.{name} is not available: fixtures must not depend on it")
+
+
+def _load_models():
+    """Import the reference's pose_net_* modules with the refusing placeholder."""
+    tv = _Refuse("torchvision")
+    tvm = _Refuse("torchvision.models")
+    saved = {k: sys.modules.get(k) for k in ("torchvision", "torchvision.models")}
+    sys.modules["torchvision"], sys.modules["torchvision.models"] = tv, tvm
+    object.__setattr__(tv, "models", tvm)
+    try:
+        rgbd = _load("ref_pose_net_rgbd", "models/pose_net_rgbd.py")
+        rgbd_geo = _load("ref_pose_net_rgbd_geometric", "models/pose_net_rgbd_geometric.py")
+        rgb_geo = _load("ref_pose_net_rgb_geometric", "models/pose_net_rgb_geometric.py")
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    return rgbd, rgbd_geo, rgb_geo
+
+
+def gen_model_parts():
+    """Outputs and gradients of the reference's own torchvision-free model code."""
+    rgbd, rgbd_geo, rgb_geo = _load_models()
+    out = {}
+    # --- CrossModalAttention (pose_net_rgbd.py:8-35), eval mode (dropout off) ------
+    # weights from a documented generator (xattn_weights, regenerated by the tests and
+    # checked against the stored checksum) instead of 64 MB of fixture
+    for name, (B, D, heads) in {"xattn": (2, 2048, 8), "xattn_small": (3, 64, 4)}.items():
+        att = rgbd.CrossModalAttention(D, num_heads=heads, dropout=0.1).eval()
+        sd = xattn_weights(D, seed=D + heads)
+        att.load_state_dict(sd)
+        g = torch.Generator().manual_seed(B * 100 + D)
+        r = (torch.randn(B, D, generator=g)).requires_grad_(True)
+        d = (torch.randn(B, D, generator=g) * 0.7 + 0.1).requires_grad_(True)
+        y = att(r, d)
+        w = torch.randn(B, D, generator=g)
+        (y * w).sum().backward()
+        out[f"{name}/weights_checksum"] = np.asarray([float(v.numpy().astype(np.float64).sum())
+                                                      for v in sd.values()], np.float64)
+        out[f"{name}/heads"] = np.asarray(heads, np.int32)
+        out[f"{name}/rgb_feat"], out[f"{name}/depth_feat"], out[f"{name}/dout"] = (r.detach().numpy(),
+                                                                                 d.detach().numpy(), w.numpy())
+        out[f"{name}/out"] = y.detach().numpy()
+        out[f"{name}/grad_rgb"], out[f"{name}/grad_depth"] = r.grad.numpy(), d.grad.numpy()
+        for k, p in att.named_parameters():
+            gr = p.grad.numpy()
+            # weight gradients: the first 16 rows and the norm of the whole (bias grads whole)
+            out[f"{name}/grad/{k}"] = gr[:16] if gr.ndim == 2 else gr
+            out[f"{name}/gradnorm/{k}"] = np.asarray(np.linalg.norm(gr.astype(np.float64)), np.float64)
+    # --- PoseNetRGBDGeometric._compute_pinhole_translation (:56-85) -----------------
+    # `self` is unused by the method: called unbound on the reference's own function
+    pin = rgbd_geo.PoseNetRGBDGeometric._compute_pinhole_translation
+    g = torch.Generator().manual_seed(21)
+    B = 16
+    # piecewise-constant 8x8 blocks (compact fixture): < 0.01, in range, > 2.0
+    depth = torch.rand(B, 28, 28, generator=g) * 2.4 - 0.2
+    depth[depth.abs() < 0.05] = 0.0
+    depth = depth.repeat_interleave(8, 1).repeat_interleave(8, 2).contiguous()
+    bbox = torch.rand(B, 2, generator=g) * 300 - 40               # incl. < 0 and > 223
+    bbox[0] = torch.tensor([223.9, 223.999])
+    bbox[1] = torch.tensor([0.0, -0.5])
+    bbox[2] = torch.tensor([112.5, 57.25])
+    depth[2, 57, 112] = 0.0                                        # the z > 0.01 branch at a sampled pixel
+    depth[3, :, :] = 5.0                                           # clamp at 2.0
+    depth[4, :, :] = 0.05                                          # clamp at 0.1
+    Kb = torch.zeros(B, 3, 3)
+    Kb[:, 0, 0] = torch.rand(B, generator=g) * 800 + 300
+    Kb[:, 1, 1] = torch.rand(B, generator=g) * 800 + 300
+    Kb[:, 0, 2] = torch.rand(B, generator=g) * 224
+    Kb[:, 1, 2] = torch.rand(B, generator=g) * 224
+    Kb[:, 2, 2] = 1.0
+    out["pin_depth/depth_raw"], out["pin_depth/bbox"], out["pin_depth/K"] = depth.numpy(), bbox.numpy(), Kb.numpy()
+    out["pin_depth/out_Kb"] = pin(None, depth, bbox, Kb).numpy()
+    out["pin_depth/out_K2"] = pin(None, depth, bbox, Kb[5]).numpy()     # a single (3, 3) K, expanded
+    # --- PoseNetRGBGeometric._compute_pinhole_translation (:93-109), with grad ---------
+    pinz = rgb_geo.PoseNetRGBGeometric._compute_pinhole_translation
+    z = (torch.randn(B, 1, generator=g) * 0.3 + 0.8).requires_grad_(True)
+    bb = torch.rand(B, 2, generator=g) * 640 - 20
+    t = pinz(None, z, bb, Kb)
+    wt = torch.randn(B, 3, generator=g)
+    (t * wt).sum().backward()
+    out["pin_z/z"], out["pin_z/bbox"], out["pin_z/K"], out["pin_z/dout"] = (z.detach().numpy(), bb.numpy(),
+                                                                           Kb.numpy(), wt.numpy())
+    out["pin_z/out_Kb"], out["pin_z/grad_z"] = t.detach().numpy(), z.grad.numpy()
+    out["pin_z/out_K2"] = pinz(None, z.detach(), bb, Kb[7]).numpy()
+    np.savez_compressed(os.path.join(OUT, "model_parts.npz"), **out)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(1)
@@ -198,6 +302,7 @@ def main():
     ref_al = _load("ref_add_loss", "models/add_loss.py")
     gen_pose_loss(ref_pl)
     gen_add(ref_al)
+    gen_model_parts()
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 
