@@ -101,24 +101,30 @@ __device__ __forceinline__ int64_t out_row(const Geom& g, int cls, int m) {
 // (+ residual).  Must be entered after a barrier that ends all LDS reads.
 // ACT: the eval BN-act store (Geom::act) compiled in (1) or out (0): the launchers
 // instantiate both, so the training kernels carry no trace of it
-template <typename T, int BM, int BN, bool BNF = false, int ACT = 0>
-__device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], char* smem, const Geom& g,
+// NW waves per workgroup: WM = NW / 2 along M times 2 along N, each wave owning a
+// (BM / WM) x (BN / 2) block of 16x16 MFMA tiles (TM x TN of them)
+template <int NW> struct WaveGrid { static constexpr int WM = NW / 2, WN = 2, NT = 64 * NW; };
+
+template <typename T, int BM, int BN, bool BNF = false, int ACT = 0, int NW = 4>
+__device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / (16 * (NW / 2))][BN / 32], char* smem, const Geom& g,
                                               const float* __restrict__ bias, const T* __restrict__ res,
                                               T* __restrict__ out, float* __restrict__ stats, int m0, int n0,
                                               int cls = -1, const BnBwd* bn = nullptr, int prow = 0) {
-  constexpr int TM = BM / 32, TN = BN / 32;
+  constexpr int WM = WaveGrid<NW>::WM, NT = WaveGrid<NW>::NT;
+  constexpr int TM = BM / (16 * WM), TN = BN / 32;
+  static_assert(TM % 2 == 0, "BatchNorm partials cover 32-row blocks of one wave");
   constexpr int CROW = BN * (int)sizeof(T) + 16;  // epilogue tile row stride (bytes)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // BN-backward epilogue: the BN's y (and forward output) chunks this thread will
   // need in the store loop are fetched first, so their latency overlaps the
   // staging below instead of serialising behind each store
-  constexpr int kBnIt = (BM * (BN * (int)sizeof(T) / 16) + kThreads - 1) / kThreads;
+  constexpr int kBnIt = (BM * (BN * (int)sizeof(T) / 16) + NT - 1) / NT;
   uint4 pre_y[BNF ? kBnIt : 1], pre_o[BNF ? kBnIt : 1];
   if constexpr (BNF) {
     constexpr int CPR0 = BN * (int)sizeof(T) / 16;
 #pragma unroll
     for (int it = 0; it < kBnIt; ++it) {
-      const int idx = tid + it * kThreads;
+      const int idx = tid + it * NT;
       const int lr = idx / CPR0, cc = idx - lr * CPR0;
       const int m = m0 + lr, c = n0 + cc * (16 / (int)sizeof(T));
       pre_y[it] = pre_o[it] = uint4{0, 0, 0, 0};
@@ -131,7 +137,7 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], ch
   }
   const int wm = wave >> 1, wn = wave & 1;
   const int fr = lane & 15, fc = lane >> 4;
-  const int row_base = m0 + wm * (BM / 2);
+  const int row_base = m0 + wm * (BM / WM);
   const int col_base = n0 + wn * (BN / 2);
   if (bias) {
 #pragma unroll
@@ -193,14 +199,14 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], ch
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int lr = wm * (BM / 2) + i * 16 + fc * 4 + r;
+        const int lr = wm * (BM / WM) + i * 16 + fc * 4 + r;
         const int lc = wn * (BN / 2) + j * 16 + fr;
         *reinterpret_cast<T*>(smem + lr * CROW + lc * (int)sizeof(T)) = p6::from_f<T>(acc[i][j][r]);
       }
   __syncthreads();
   constexpr int CPR = BN * (int)sizeof(T) / 16;  // 16-B chunks per tile row
   constexpr int E = 16 / (int)sizeof(T);
-  constexpr bool kBnOk = BNF && sizeof(T) == 2 && CPR == 8 && kThreads % CPR == 0;
+  constexpr bool kBnOk = BNF && sizeof(T) == 2 && CPR == 8 && NT == 256;
   static_assert(!BNF || kBnOk, "BN-backward epilogue: bf16 64-column tiles only");
   const bool bnf = kBnOk;
   float bs[E], bq[E];
@@ -208,7 +214,7 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], ch
   for (int e = 0; e < E; ++e) bs[e] = bq[e] = 0.f;
   // eval BN-act: a thread's 16-B chunk column (tid % CPR) is the same on every store
   // iteration, so its channels' constants are loaded once
-  static_assert(kThreads % CPR == 0, "store loop: fixed chunk column per thread");
+  static_assert(NT % CPR == 0, "store loop: fixed chunk column per thread");
   float asc[E], ash[E], arsc[E], arsh[E];
   constexpr bool act = ACT == 1;
   if (act) {
@@ -223,8 +229,8 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / 32][BN / 32], ch
     }
   }
 #pragma unroll
-  for (int it = 0; it < (BM * CPR + kThreads - 1) / kThreads; ++it) {
-    const int idx = tid + it * kThreads;
+  for (int it = 0; it < (BM * CPR + NT - 1) / NT; ++it) {
+    const int idx = tid + it * NT;
     if (idx >= BM * CPR) break;
     const int lr = idx / CPR, cc = idx - lr * CPR;
     const int m = m0 + lr, c = n0 + cc * E;
@@ -563,21 +569,48 @@ __device__ __forceinline__ void lds_wait_all(u32x4 (&f)[4]) {
   asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
 }
 
+// one 16-byte fragment pair -> the 16x16 accumulator: bf16 = one 16x16x32 MFMA,
+// fp32 = four exact 16x16x4 MFMAs (component s of every lane's chunk)
+template <typename T>
+__device__ __forceinline__ void mma_frag(f32x4& acc, const u32x4& a, const u32x4& b) {
+  if constexpr (sizeof(T) == 2) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc, 0,
+                                                  0, 0);
+  } else {
+    const f32x4 a4 = __builtin_bit_cast(f32x4, a), b4 = __builtin_bit_cast(f32x4, b);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[s], b4[s], acc, 0, 0, 0);
+  }
+}
+
 #ifndef POSE6D_PAIRED_FRAGS
 #define POSE6D_PAIRED_FRAGS 1
 #endif
 constexpr bool kPairedFrags = POSE6D_PAIRED_FRAGS;
 
+// Element geometry of the LDS-DMA path: a 16-byte chunk holds CH elements, a K-step
+// (one 128-byte LDS row per GEMM row) KS = 8 CH: 64 bf16 or 32 fp32.  bf16 feeds
+// v_mfma_f32_16x16x32_bf16 (one per 16x16 tile and k-half); fp32 feeds the exact
+// v_mfma_f32_16x16x4_f32, four per tile and k-half -- a lane's 16-byte chunk holds
+// k = 4 (fc + 4 kk) + s, s = 0..3, for A and B alike, so MFMA s sums the same k.
+template <typename T> struct LK { static constexpr int CH = 16 / (int)sizeof(T), KS = 8 * CH; };
+
 // one workgroup's work; `bid_in` = its index in this conv's sub-grid (the whole grid,
 // or the leading part of a fused backward launch), `smem` = the kernel's dynamic LDS
-template <int BM, int BN, int MODE, int S, bool BNF = false, bool ACT = false>
-__device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16* __restrict__ src,
-                                              const bf16* __restrict__ wts, const float* __restrict__ bias,
-                                              const bf16* __restrict__ res, bf16* __restrict__ out,
+template <typename T, int BM, int BN, int MODE, int S, bool BNF = false, bool ACT = false, int NW = 4>
+__device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* __restrict__ src,
+                                              const T* __restrict__ wts, const float* __restrict__ bias,
+                                              const T* __restrict__ res, T* __restrict__ out,
                                               float* __restrict__ stats, const Geom& g,
                                               const BnBwd* bn = nullptr) {
-  constexpr int TM = BM / 32, TN = BN / 32;
-  constexpr int A_INS = BM / 32, B_INS = BN / 32;   // DMA instructions per thread per stage
+  constexpr int CH = LK<T>::CH, KS = LK<T>::KS;
+  static_assert(KS == 64 || KS == 32, "bf16 or fp32");
+  constexpr int LOG_KS = KS == 64 ? 6 : 5;
+  constexpr int WM = WaveGrid<NW>::WM;
+  constexpr int TM = BM / (16 * WM), TN = BN / 32;
+  constexpr int RW = 8 * NW;                        // rows one DMA instruction of every wave covers
+  constexpr int A_INS = BM / RW, B_INS = BN / RW;   // DMA instructions per thread per stage
+  static_assert(A_INS * RW == BM && B_INS * RW == BN, "tile rows must be a multiple of 8 x waves");
   constexpr int LOADS = A_INS + B_INS;
   constexpr int SA = BM * 128, STAGE = (BM + BN) * 128;
   static_assert(S >= 2, "ring needs two stages");
@@ -592,7 +625,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
   // parity class (kDgradS2): the four classes of one tile are consecutive logical
   // ids, so every XCD gets an even share of the heavy and the empty classes and the
   // four blocks that gather the same dY rows run on the same L2
-  int cls = -1, py = 0, px = 0, kh0 = 0, kw0 = 0, ntx = 1, nk = g.Kpad >> 6;
+  int cls = -1, py = 0, px = 0, kh0 = 0, kw0 = 0, ntx = 1, nk = g.Kpad >> LOG_KS;
   if (MODE == kDgradS2) {
     if (g.s2one) {
       cls = g.s2one - 1;
@@ -604,7 +637,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
     kh0 = (py + g.pad) & 1; kw0 = (px + g.pad) & 1;   // first tap of this parity, then every 2nd
     const int nty = (g.KH - kh0 + 1) >> 1;
     ntx = (g.KW - kw0 + 1) >> 1;
-    nk = (nty * ntx) << (g.log2SC - 6);
+    nk = (nty * ntx) << (g.log2SC - LOG_KS);
     // a class no tap reaches (1x1 stride 2: three of four) contributes zeros: with
     // the residual accumulated in place (res == out) its pixels are already final
     if (nk == 0 && res == out) return;
@@ -620,15 +653,15 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
   const int r8 = lane >> 3, pch = lane & 7;
   const char* zp = reinterpret_cast<const char*>(g_zero_page);
 
-  // rows this lane DMAs: row = i*32 + wave*8 + r8; it fetches logical chunk pch ^ swz8(row)
+  // rows this lane DMAs: row = i*RW + wave*8 + r8; it fetches logical chunk pch ^ swz8(row)
   int a_pix[A_INS], a_y[A_INS], a_x[A_INS], a_ck[A_INS];
   bool a_ok[A_INS];
 #pragma unroll
   for (int i = 0; i < A_INS; ++i) {
-    const int row = i * 32 + wave * 8 + r8;
+    const int row = i * RW + wave * 8 + r8;
     const int m = m0 + row;
     a_ok[i] = m < g.M;
-    a_ck[i] = (pch ^ swz8(row)) * 8;
+    a_ck[i] = (pch ^ swz8(row)) * CH;
     const int mm = a_ok[i] ? m : 0;
     if (MODE == kGemm) {
       a_pix[i] = mm; a_y[i] = 0; a_x[i] = 0;
@@ -643,14 +676,14 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
     }
   }
   // B rows: n >= Ncols read the zero page (offset masked to 0)
-  const bf16* b_base[B_INS];
+  const T* b_base[B_INS];
   unsigned b_mask[B_INS];
 #pragma unroll
   for (int j = 0; j < B_INS; ++j) {
-    const int row = j * 32 + wave * 8 + r8;
+    const int row = j * RW + wave * 8 + r8;
     const int n = n0 + row;
     const bool ok = n < g.Ncols;
-    b_base[j] = ok ? wts + (int64_t)n * g.Kpad + (pch ^ swz8(row)) * 8 : reinterpret_cast<const bf16*>(zp);
+    b_base[j] = ok ? wts + (int64_t)n * g.Kpad + (pch ^ swz8(row)) * CH : reinterpret_cast<const T*>(zp);
     b_mask[j] = ok ? ~0u : 0u;
   }
 
@@ -662,7 +695,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
   // workgroup per CU.  issue() is called with consecutive kt.
   const int tap_len = MODE == kGemm ? g.Kpad : g.SC;
   int c0 = 0, kh = kh0, kw = kw0, tw = 0, tap_koff = MODE == kDgradS2 ? (kh0 * g.KW + kw0) * g.SC : 0;
-  const bf16* a_base[A_INS];
+  const T* a_base[A_INS];
   unsigned a_mask[A_INS];
   auto set_tap = [&]() {
 #pragma unroll
@@ -688,7 +721,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
         ok = ok && (unsigned)sy < (unsigned)g.SH && (unsigned)sx < (unsigned)g.SW;
         off = (int64_t)(a_pix[i] + sy * g.SW + sx) << g.log2SC;
       }
-      a_base[i] = ok ? src + off + a_ck[i] : reinterpret_cast<const bf16*>(zp);
+      a_base[i] = ok ? src + off + a_ck[i] : reinterpret_cast<const T*>(zp);
       a_mask[i] = ok ? ~0u : 0u;
     }
   };
@@ -700,10 +733,10 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
     if (c0 == 0) set_tap();
     const unsigned boff = (unsigned)(tap_koff + c0);
 #pragma unroll
-    for (int j = 0; j < B_INS; ++j) glds16(b_base[j] + (boff & b_mask[j]), Bs + (j * 32 + wave * 8) * 128);
+    for (int j = 0; j < B_INS; ++j) glds16(b_base[j] + (boff & b_mask[j]), Bs + (j * RW + wave * 8) * 128);
 #pragma unroll
-    for (int i = 0; i < A_INS; ++i) glds16(a_base[i] + ((unsigned)c0 & a_mask[i]), As + (i * 32 + wave * 8) * 128);
-    c0 += 64;
+    for (int i = 0; i < A_INS; ++i) glds16(a_base[i] + ((unsigned)c0 & a_mask[i]), As + (i * RW + wave * 8) * 128);
+    c0 += KS;
     if (c0 == tap_len) {
       c0 = 0;
       if (MODE == kDgradS2) {
@@ -730,7 +763,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
   for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int row = wm * (BM / 2) + i * 16 + fr;
+      const int row = wm * (BM / WM) + i * 16 + fr;
       frag_off[kk][i] = row * 128 + (((fc + 4 * kk) ^ swz8(row)) << 4);
     }
 #pragma unroll
@@ -760,10 +793,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f[kk][i]),
-                                                                __builtin_bit_cast(bf16x8, f[kk][TM + j]), acc[i][j],
-                                                                0, 0, 0);
+          for (int j = 0; j < TN; ++j) mma_frag<T>(acc[i][j], f[kk][i], f[kk][TM + j]);
       }
       return;
     }
@@ -778,10 +808,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f[i]),
-                                                              __builtin_bit_cast(bf16x8, f[TM + j]), acc[i][j], 0, 0,
-                                                              0);
+        for (int j = 0; j < TN; ++j) mma_frag<T>(acc[i][j], f[i], f[TM + j]);
     }
   };
 
@@ -798,17 +825,17 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const bf16
     wbuf = wbuf == S - 1 ? 0 : wbuf + 1;
   }
   asm volatile("s_barrier" ::: "memory");   // every wave done reading the ring before the epilogue reuses it
-  conv_epilogue<bf16, BM, BN, BNF, ACT ? 1 : 0>(acc, smem, g, bias, res, out, stats, m0, n0, cls, bn,
+  conv_epilogue<T, BM, BN, BNF, ACT ? 1 : 0, NW>(acc, smem, g, bias, res, out, stats, m0, n0, cls, bn,
                                    MODE == kDgradS2 ? tm * 4 + cls : tm);
 }
 
-template <int BM, int BN, int MODE, int S, bool ACT>
-__global__ __launch_bounds__(kThreads) void conv_lds_kernel(const bf16* __restrict__ src, const bf16* __restrict__ wts,
-                                                            const float* __restrict__ bias,
-                                                            const bf16* __restrict__ res, bf16* __restrict__ out,
-                                                            float* __restrict__ stats, Geom g) {
+template <typename T, int BM, int BN, int MODE, int S, bool ACT, int NW>
+__global__ __launch_bounds__(64 * NW) void conv_lds_kernel(const T* __restrict__ src, const T* __restrict__ wts,
+                                                           const float* __restrict__ bias,
+                                                           const T* __restrict__ res, T* __restrict__ out,
+                                                           float* __restrict__ stats, Geom g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv_lds_body<BM, BN, MODE, S, false, ACT>(smem, blockIdx.x, src, wts, bias, res, out, stats, g);
+  conv_lds_body<T, BM, BN, MODE, S, false, ACT, NW>(smem, blockIdx.x, src, wts, bias, res, out, stats, g);
 }
 
 // Fused backward of one conv: workgroups [0, nd) compute the data gradient,
@@ -826,7 +853,7 @@ __global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const bf16* __restri
   const int b = blockIdx.x;
   const int nw = gw.gm * gw.gn * gw.splits;
   if (b < nd_pad) {
-    if (b < nd) conv_lds_body<64, 64, DMODE, DS, BNF>(smem, b, dy, wt, nullptr, dres, dx, nullptr, gd, &bn);
+    if (b < nd) conv_lds_body<bf16, 64, 64, DMODE, DS, BNF>(smem, b, dy, wt, nullptr, dres, dx, nullptr, gd, &bn);
   } else if (b < nd_pad + nw) {
     conv_wgrad_lds_body<64, 64, WS>(smem, b - nd_pad, x, dy, ws, gw);
   } else {
@@ -836,16 +863,17 @@ __global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const bf16* __restri
   }
 }
 
-// K-steps of the longest work item (kDgradS2: the class with the most taps)
-int fast_nk(int mode, const Geom& g) {
-  if (mode != kDgradS2) return g.Kpad / 64;
+// K-steps of the longest work item (kDgradS2: the class with the most taps);
+// ks = elements per K-step (64 bf16, 32 fp32)
+int fast_nk(int mode, const Geom& g, int ks = 64) {
+  if (mode != kDgradS2) return g.Kpad / ks;
   int best = 0;
   for (int cls = 0; cls < 4; ++cls) {
     const int kh0 = ((cls >> 1) + g.pad) & 1, kw0 = ((cls & 1) + g.pad) & 1;
     const int t = ((g.KH - kh0 + 1) >> 1) * ((g.KW - kw0 + 1) >> 1);
     best = t > best ? t : best;
   }
-  return best * g.SC / 64;
+  return best * g.SC / ks;
 }
 
 int stage_bytes(int tile) {
@@ -853,64 +881,73 @@ int stage_bytes(int tile) {
   return (bm[tile] + bn[tile]) * 128;
 }
 
-template <int BM, int BN, int MODE, int S>
+template <typename T, int BM, int BN, int MODE, int S, int NW = 4>
 int launch_fast(const Geom& g0, const void* src, const void* w, const float* bias, const void* res, void* out,
                 float* stats, hipStream_t s) {
   Geom g = g0;
   g.gm = p6::ceil_div(g.M, BM);
   g.gn = p6::ceil_div(g.Ncols, BN);
-  const int nk = fast_nk(MODE, g);
+  const int nk = fast_nk(MODE, g, LK<T>::KS);
   const int ring = (nk < S ? (nk > 0 ? nk : 1) : S) * (BM + BN) * 128;
-  const int epi = BM * (BN * 2 + 16);
+  const int epi = BM * (BN * (int)sizeof(T) + 16);
   const int lds = ring > epi ? ring : epi;
   if (MODE == kDgradS2) s2_single_class(g, res, out);
   const int grid = g.gm * g.gn * (MODE == kDgradS2 ? s2_classes(g) : 1);
   if constexpr (MODE == kGemm || MODE == kFwd) {
     if (g.act) {   // eval BN-act epilogue (pose6d_conv2d_fwd_act)
-      conv_lds_kernel<BM, BN, MODE, S, true><<<grid, kThreads, lds, s>>>((const bf16*)src, (const bf16*)w, bias,
-                                                                         (const bf16*)res, (bf16*)out, stats, g);
+      conv_lds_kernel<T, BM, BN, MODE, S, true, NW><<<grid, 64 * NW, lds, s>>>((const T*)src, (const T*)w, bias,
+                                                                               (const T*)res, (T*)out, stats, g);
       P6_LAUNCH_CHECK();
       return POSE6D_OK;
     }
   }
-  conv_lds_kernel<BM, BN, MODE, S, false><<<grid, kThreads, lds, s>>>((const bf16*)src, (const bf16*)w, bias,
-                                                                       (const bf16*)res, (bf16*)out, stats, g);
+  conv_lds_kernel<T, BM, BN, MODE, S, false, NW><<<grid, 64 * NW, lds, s>>>((const T*)src, (const T*)w, bias,
+                                                                             (const T*)res, (T*)out, stats, g);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
 
-template <int BM, int BN, int MODE>
+template <typename T, int BM, int BN, int MODE, int NW = 4>
 int launch_fast_s(const Geom& g, int stages, const void* src, const void* w, const float* bias, const void* res,
                   void* out, float* stats, hipStream_t s) {
   switch (stages) {
-    case 2: return launch_fast<BM, BN, MODE, 2>(g, src, w, bias, res, out, stats, s);
-    case 3: return launch_fast<BM, BN, MODE, 3>(g, src, w, bias, res, out, stats, s);
-    case 4: return launch_fast<BM, BN, MODE, 4>(g, src, w, bias, res, out, stats, s);
+    case 2: return launch_fast<T, BM, BN, MODE, 2, NW>(g, src, w, bias, res, out, stats, s);
+    case 3: return launch_fast<T, BM, BN, MODE, 3, NW>(g, src, w, bias, res, out, stats, s);
+    case 4: return launch_fast<T, BM, BN, MODE, 4, NW>(g, src, w, bias, res, out, stats, s);
     default:
-      if constexpr ((BM + BN) * 128 * 6 <= 160 * 1024) return launch_fast<BM, BN, MODE, 6>(g, src, w, bias, res, out,
-                                                                                           stats, s);
-      else return launch_fast<BM, BN, MODE, 4>(g, src, w, bias, res, out, stats, s);
+      if constexpr ((BM + BN) * 128 * 6 <= 160 * 1024) return launch_fast<T, BM, BN, MODE, 6, NW>(g, src, w, bias,
+                                                                                                  res, out, stats, s);
+      else return launch_fast<T, BM, BN, MODE, 4, NW>(g, src, w, bias, res, out, stats, s);
   }
 }
 
-template <int MODE>
+template <typename T, int MODE>
 int launch_fast_mode(const Geom& g, int tile, int stages, const void* src, const void* w, const float* bias,
                      const void* res, void* out, float* stats, hipStream_t s) {
   switch (tile) {
-    case 0: return launch_fast_s<128, 128, MODE>(g, stages, src, w, bias, res, out, stats, s);
-    case 1: return launch_fast_s<128, 64, MODE>(g, stages, src, w, bias, res, out, stats, s);
-    default: return launch_fast_s<64, 64, MODE>(g, stages, src, w, bias, res, out, stats, s);
+    case 0: return launch_fast_s<T, 128, 128, MODE>(g, stages, src, w, bias, res, out, stats, s);
+    case 1: return launch_fast_s<T, 128, 64, MODE>(g, stages, src, w, bias, res, out, stats, s);
+    case 4: return launch_fast_s<T, 128, 128, MODE, 8>(g, stages, src, w, bias, res, out, stats, s);
+    case 5: return launch_fast_s<T, 128, 64, MODE, 8>(g, stages, src, w, bias, res, out, stats, s);
+    default: return launch_fast_s<T, 64, 64, MODE>(g, stages, src, w, bias, res, out, stats, s);
   }
 }
 
-int dispatch_fast(int mode, const Geom& g, int tile, int stages, const void* src, const void* w, const float* bias,
-                  const void* res, void* out, float* stats, hipStream_t s) {
+template <typename T>
+int dispatch_fast_t(int mode, const Geom& g, int tile, int stages, const void* src, const void* w, const float* bias,
+                    const void* res, void* out, float* stats, hipStream_t s) {
   switch (mode) {
-    case kGemm: return launch_fast_mode<kGemm>(g, tile, stages, src, w, bias, res, out, stats, s);
-    case kFwd: return launch_fast_mode<kFwd>(g, tile, stages, src, w, bias, res, out, stats, s);
-    case kDgradS2: return launch_fast_mode<kDgradS2>(g, tile, stages, src, w, bias, res, out, stats, s);
-    default: return launch_fast_mode<kDgrad>(g, tile, stages, src, w, bias, res, out, stats, s);
+    case kGemm: return launch_fast_mode<T, kGemm>(g, tile, stages, src, w, bias, res, out, stats, s);
+    case kFwd: return launch_fast_mode<T, kFwd>(g, tile, stages, src, w, bias, res, out, stats, s);
+    case kDgradS2: return launch_fast_mode<T, kDgradS2>(g, tile, stages, src, w, bias, res, out, stats, s);
+    default: return launch_fast_mode<T, kDgrad>(g, tile, stages, src, w, bias, res, out, stats, s);
   }
+}
+
+int dispatch_fast(int dtype, int mode, const Geom& g, int tile, int stages, const void* src, const void* w,
+                  const float* bias, const void* res, void* out, float* stats, hipStream_t s) {
+  return dtype == POSE6D_DT_BF16 ? dispatch_fast_t<bf16>(mode, g, tile, stages, src, w, bias, res, out, stats, s)
+                                 : dispatch_fast_t<float>(mode, g, tile, stages, src, w, bias, res, out, stats, s);
 }
 
 template <typename T, int BM, int BN, int MODE>
@@ -982,22 +1019,34 @@ extern "C" int pose6d_conv_stats_rows(int32_t N, int32_t Ho, int32_t Wo, int32_t
   return p6::ceil_div((int64_t)N * Ho * Wo, 32);
 }
 
-// implementation choice: the LDS-DMA fast path for bf16 whenever each 64-deep K slice
-// lies inside one filter tap; the register-staged kernel otherwise (fp32, stem,
-// 32-channel z-CNN).  POSE6D_CONV_IMPL=base|fast and POSE6D_CONV_TILE=0..3 override
+int env_int(const char* name, int dflt);
+
+// implementation choice: the LDS-DMA fast path whenever each 128-byte K slice (64
+// bf16 / 32 fp32 channels) lies inside one filter tap; the register-staged kernel
+// otherwise (the Cin-4 stem, the 3- and 32-channel z-CNN layers).
+// POSE6D_CONV_F32_FAST=0 keeps fp32 on the register-staged kernel (A/B only).  POSE6D_CONV_IMPL=base|fast and POSE6D_CONV_TILE=0..3 override
 // (tuning / A-B experiments only).
 bool fast_ok(int dtype, int mode, const Geom& g) {
-  if (dtype != POSE6D_DT_BF16 || mode == kFwdNarrow) return false;
-  if (g.K % 64 != 0 || g.Kpad != g.K) return false;
-  return mode == kGemm || g.SC % 64 == 0;
+  if (mode == kFwdNarrow) return false;
+  if (dtype == POSE6D_DT_F32 && env_int("POSE6D_CONV_F32_FAST", 1) == 0) return false;
+  const int ks = dtype == POSE6D_DT_BF16 ? 64 : 32;   // elements per 128-byte K-step
+  if (g.K % ks != 0 || g.Kpad != g.K) return false;
+  return mode == kGemm || g.SC % ks == 0;
 }
 
-// 64x64 tiles: measured best or within a few % on every ResNet50 layer at batch
-// 32 (tools/conv_bench.py sweep) -- occupancy beats per-wave operand reuse at
-// these grid sizes
-int pick_tile_fast(int64_t M, int N, int mult) {
-  (void)M; (void)N; (void)mult;
-  return 3;
+// Tile per GEMM shape.  The 64x64 / 4-wave tile keeps the most workgroups resident
+// and wins while K is short or the grid would get thin; a 128x128 tile on 8 waves
+// (tile 4) halves the LDS-DMA bytes per MFMA (each 32 KiB stage feeds four times
+// the MACs of a 16 KiB one), which wins inside the training step once K >= 256 and
+// the grid keeps >= 384 workgroups (layer2.0 ds / conv1, layer3.0 ds / conv1,
+// layer3 conv3: 1-3 us each).  128x64 on 8 waves (tile 5) won standalone sweeps
+// (tools/conv_bench.py) but lost in the step, so bf16 never picks it.  fp32
+// (MFMA-bound: 4x the MFMAs per byte) takes 128x128 on long K at about one
+// workgroup per CU (profiles/r02_conv_tiles.txt).
+int pick_tile_fast(int dtype, int64_t M, int N, int K) {
+  const int64_t wg4 = p6::ceil_div(M, 128) * (int64_t)p6::ceil_div(N, 128);
+  if (dtype == POSE6D_DT_F32) return (K >= 512 && N >= 128 && wg4 >= 192 && wg4 < 384) ? 4 : 3;
+  return (N >= 128 && K >= 256 && wg4 >= 384) ? 4 : 3;
 }
 
 int env_int(const char* name, int dflt) {
@@ -1017,7 +1066,8 @@ bool s2_ok(const Geom& g) {
   return g.stride == 2 && (g.RH & 1) == 0 && (g.RW & 1) == 0 && g.SH == g.RH / 2 && g.SW == g.RW / 2;
 }
 
-Plan choose(int dtype, int mode, const Geom& g) {
+// fused = the data-gradient half of conv_bwd_kernel (its workgroups are 64x64 / 4 waves)
+Plan choose(int dtype, int mode, const Geom& g, bool fused = false) {
   const char* impl = getenv("POSE6D_CONV_IMPL");
   Plan p{};
   p.fast = fast_ok(dtype, mode, g) && !(impl && strcmp(impl, "base") == 0);
@@ -1039,25 +1089,29 @@ Plan choose(int dtype, int mode, const Geom& g) {
     const char* ord = getenv("POSE6D_CONV_ORDER");
     p.g.nmajor = ord && ord[0] == 'n';
   }
-  p.tile = env_int("POSE6D_CONV_TILE", pick_tile_fast(p.g.M, g.Ncols, p.mode == kDgradS2 ? 4 : 1));
+  p.tile = fused ? 3 : env_int("POSE6D_CONV_TILE", pick_tile_fast(dtype, p.g.M, g.Ncols, g.K));
   if (p.tile == 2) p.tile = 3;   // no 64x128 instance on the fast path
   // two slots (32 KiB at 64x64) keep several workgroups per CU resident, which hides
   // the DMA latency better than a deeper ring; only long-K grids that leave CUs
   // idle (one wave of workgroups) take a 4-deep ring
-  const int64_t grid = (int64_t)p6::ceil_div(p.g.M, p.tile <= 1 ? 128 : 64) *
-                       p6::ceil_div(g.Ncols, p.tile == 0 ? 128 : 64) * (p.mode == kDgradS2 ? 4 : 1);
-  p.stages = env_int("POSE6D_CONV_STAGES", (fast_nk(p.mode, p.g) > 24 && grid <= 512) ? 4 : 2);
+  // tiles: 0 = 128x128, 1 = 128x64, 3 = 64x64 (4 waves); 4 = 128x128, 5 = 128x64 (8 waves)
+  const bool rows128 = p.tile <= 1 || p.tile == 4 || p.tile == 5;
+  const bool cols128 = p.tile == 0 || p.tile == 4;
+  const int64_t grid = (int64_t)p6::ceil_div(p.g.M, rows128 ? 128 : 64) * p6::ceil_div(g.Ncols, cols128 ? 128 : 64) *
+                       (p.mode == kDgradS2 ? 4 : 1);
+  p.stages = env_int("POSE6D_CONV_STAGES",
+                     (fast_nk(p.mode, p.g, dtype == POSE6D_DT_BF16 ? 64 : 32) > 24 && grid <= 512) ? 4 : 2);
   if (p.stages < 2) p.stages = 2;
   if (p.stages > 6) p.stages = 6;
   if (p.stages == 5) p.stages = 4;
-  if (p.tile == 0 && p.stages > 4) p.stages = 4;   // 6 x 32 KiB exceeds the 160 KiB LDS
+  if (cols128 && rows128 && p.stages > 4) p.stages = 4;   // 6 x 32 KiB exceeds the 160 KiB LDS
   return p;
 }
 
 int run_conv(int dtype, int mode, const Geom& g, const void* src, const void* w, const float* bias, const void* res,
              void* out, float* stats, hipStream_t s) {
   const Plan p = choose(dtype, mode, g);
-  if (p.fast) return dispatch_fast(p.mode, p.g, p.tile, p.stages, src, w, bias, res, out, stats, s);
+  if (p.fast) return dispatch_fast(dtype, p.mode, p.g, p.tile, p.stages, src, w, bias, res, out, stats, s);
   return dtype == POSE6D_DT_BF16 ? dispatch<bf16>(mode, g, p.tile, src, w, bias, res, out, stats, s)
                                  : dispatch<float>(mode, g, p.tile, src, w, bias, res, out, stats, s);
 }
@@ -1232,7 +1286,7 @@ extern "C" int pose6d_conv2d_bn_rows(int32_t dtype, int32_t N, int32_t H, int32_
   if (Cin % 8 != 0 || ilog2(Cin) < 3) return 0;
   int mode;
   const Geom gd0 = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
-  const Plan pd = choose(dtype, mode, gd0);
+  const Plan pd = choose(dtype, mode, gd0, true);
   p6::WgradPlan pw;
   p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
   if (!bwd_fused(pd, pw)) return 0;
@@ -1285,7 +1339,7 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
                "pose6d_conv2d_backward: Cin must be a power of two >= 8 for the data gradient");
   int mode;
   const Geom gd0 = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
-  const Plan pd = choose(dtype, mode, gd0);
+  const Plan pd = choose(dtype, mode, gd0, true);
   p6::WgradPlan pw;
   const p6::WGeom gw = p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
   const bool fused = bwd_fused(pd, pw);
@@ -1346,7 +1400,7 @@ extern "C" int pose6d_bwd_variant(int32_t dtype, int32_t N, int32_t H, int32_t W
   if (Cin % 8 != 0 || ilog2(Cin) < 3) return 0;
   int mode;
   const Geom gd0 = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
-  const Plan pd = choose(dtype, mode, gd0);
+  const Plan pd = choose(dtype, mode, gd0, true);
   p6::WgradPlan pw;
   p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
   return bwd_fused(pd, pw) ? (1 << 16) | (pd.mode << 4) | pd.stages : 0;

@@ -208,18 +208,10 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const T* __restric
       __syncthreads();
     }
   }
-  // slab write: rows co, cols k (C/D map: col = lane & 15, row = 4 * (lane >> 4) + r)
+  // slab write: rows co, cols k, staged through LDS as 16-byte row vectors (the
+  // loop's last __syncthreads ended every read of the staging buffers)
   float* slab = ws + (int64_t)split * g.Cout * g.Kpad;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wm * (BM / 2) + i * 16 + grp * 4 + r;
-        const int k = k0 + wn * (BN / 2) + j * 16 + li;
-        if (co < g.Cout && k < g.Kpad) slab[(int64_t)co * g.Kpad + k] = acc[i][j][r];
-      }
+  store_acc_tile<BM, BN, true>(acc, smem, slab + (int64_t)co0 * g.Kpad + k0, g.Kpad, g.Cout - co0, g.Kpad - k0);
 }
 
 
@@ -311,6 +303,7 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC) {
 
 template <int S>
 int launch_fast(const WGeom& g, const void* x, const void* dy, float* ws, hipStream_t s) {
+  static_assert(S * (64 + 64) * 128 >= acc_stage_bytes<64, 64>(), "ring too small to stage the tile");
   const int lds = S * (64 + 64) * 128;
   conv_wgrad_lds_kernel<S><<<g.gm * g.gn * g.splits, kThreads, lds, s>>>((const bf16*)x, (const bf16*)dy, ws, g);
   P6_LAUNCH_CHECK();
@@ -319,7 +312,8 @@ int launch_fast(const WGeom& g, const void* x, const void* dy, float* ws, hipStr
 
 template <typename T, int BM, int BN>
 int launch(const WGeom& g, const void* x, const void* dy, float* ws, hipStream_t s) {
-  const int lds = 2 * MT * (BM + BN) * (int)sizeof(T);
+  const int ring = 2 * MT * (BM + BN) * (int)sizeof(T);
+  const int lds = ring > acc_stage_bytes<BM, BN>() ? ring : acc_stage_bytes<BM, BN>();
   conv_wgrad_kernel<T, BM, BN><<<g.gm * g.gn * g.splits, kThreads, lds, s>>>((const T*)x, (const T*)dy, ws, g);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;

@@ -30,6 +30,45 @@ int wgrad_reduce_launch(const float* ws, float* dw, int Cout, int Kpad, int SC, 
 
 namespace {
 
+// fp32 accumulator tile (4 waves as 2 x 2, each BM/2 x BN/2 of 16x16 MFMA tiles:
+// lane (li, grp) holds rows 4 grp + r, column li) -> dst rows [0, BM) x cols [0, BN)
+// (row stride ld), through LDS so the global stores are whole 16-byte vectors of
+// contiguous columns: 4 (64x64) instead of 64 scattered dword stores per lane --
+// the dword form made the weight-gradient slab epilogue store-issue bound.
+// Entered after a barrier that ends every read of `smem`; needs BM * (BN + 16) * 4
+// bytes of it.  CHECK: clip rows >= rows / cols >= cols (partial tiles).
+template <int BM, int BN>
+constexpr int acc_stage_bytes() { return BM * (BN + 16) * 4; }
+
+template <int BM, int BN, bool CHECK>
+__device__ __forceinline__ void store_acc_tile(const f32x4 (&acc)[BM / 32][BN / 32], char* smem, float* dst,
+                                               int64_t ld, int rows, int cols) {
+  constexpr int TM = BM / 32, TN = BN / 32;
+  constexpr int LDT = BN + 16;              // floats per LDS row: rows alternate 16-bank halves
+  float* t = reinterpret_cast<float*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int grp = lane >> 4, li = lane & 15;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        t[(wm * (BM / 2) + i * 16 + grp * 4 + r) * LDT + wn * (BN / 2) + j * 16 + li] = acc[i][j][r];
+  __syncthreads();
+  constexpr int CPR = BN / 4;               // float4 per row
+  constexpr int RPP = 256 / CPR;            // rows per pass
+  const int c4 = tid % CPR, r0 = tid / CPR;
+#pragma unroll
+  for (int pass = 0; pass < BM / RPP; ++pass) {
+    const int row = pass * RPP + r0;
+    const float4 v = *reinterpret_cast<const float4*>(t + row * LDT + c4 * 4);
+    if (CHECK && (row >= rows || c4 * 4 >= cols)) continue;
+    *reinterpret_cast<float4*>(dst + (int64_t)row * ld + c4 * 4) = v;
+  }
+}
+
 // ============================================================================
 // Fast path (bf16, Cin a multiple of 64, Cout a multiple of 64): each stage is
 // 64 pixels deep; dY [64 m][64 co] and X [64 m][64 k] sub-images (one filter tap,
@@ -256,17 +295,11 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
     wbuf = wbuf == S - 1 ? 0 : wbuf + 1;
   }
 
+  // every wave is done reading the ring (and every DMA has landed: the last
+  // wait_ahead waited for all of them) before the tile is staged over it
+  asm volatile("s_barrier" ::: "memory");
   float* slab = ws + (int64_t)split * g.Cout * g.Kpad;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wm * (BM / 2) + i * 16 + grp * 4 + r;
-        const int k = k0 + wn * (BN / 2) + j * 16 + li;
-        slab[(int64_t)co * g.Kpad + k] = acc[i][j][r];
-      }
+  store_acc_tile<BM, BN, false>(acc, smem, slab + (int64_t)co0 * g.Kpad + k0, g.Kpad, BM, BN);
 }
 
 

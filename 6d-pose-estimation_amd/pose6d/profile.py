@@ -7,7 +7,8 @@ import torch
 
 from ._lib import call, query, stream
 
-TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}
+# pose6d_conv_variant tile codes -> (BM, BN, waves per workgroup)
+TILES = {0: (128, 128, 4), 1: (128, 64, 4), 2: (64, 128, 4), 3: (64, 64, 4), 4: (128, 128, 8), 5: (128, 64, 8)}
 
 
 def _tname(dtype):
@@ -15,10 +16,10 @@ def _tname(dtype):
 
 
 def _sym(v, T):
-    bm, bn = TILES[v & 15]
+    bm, bn, nw = TILES[v & 15]
     mode = (v >> 4) & 15
     if (v >> 8) & 1:
-        return f"conv_lds_kernel<{bm}, {bn}, {mode}, {v >> 12}, false>"
+        return f"conv_lds_kernel<{T}, {bm}, {bn}, {mode}, {v >> 12}, false, {nw}>"
     return f"conv_igemm_kernel<{T}, {bm}, {bn}, {mode}, false>"
 
 

@@ -32,6 +32,10 @@ PEAK_HBM_GBS = 8000.0       # HBM3E spec
 FWD_BYTES_PER_CROP = 58.45e6   # bf16 fused-ideal forward bytes / crop
 FWD_BYTES_PER_CROP_F32 = 116.89e6   # the same forward in fp32
 PEAK_F32_VALU_TFLOPS = 157.3   # MI355X fp32 vector peak
+PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X fp32 MFMA peak = the vector rate (MI355X_MICROARCH.md)
+# PoseNetRGB forward FLOPs per crop: ResNet50 trunk 8.175 G + the two
+# 2048-2048-1024-512-{4,3} heads (13.64 M multiply-adds)
+RGB_FWD_FLOPS_PER_CROP = 8.175e9 + 2 * 13_635_072
 ADD_FLOPS_PER_PAIR = 8.0       # 3 sub, 1 mul, 2 fma per ADD-S pair
 
 
@@ -235,7 +239,7 @@ def main():
     if rank == 0 and not args.no_kernel_profile:
         result.update(kernel_profile(tr, ms))
     if rank == 0 and not args.no_side:
-        result["side_configs"] = {"configs[1]": rgb_fp32_forward(dev),
+        result["side_configs"] = {"configs[1]": rgb_fp32_forward(dev), "dropin_fp32_train": dropin_fp32_train(dev),
                                   "configs[3]": add_eval_throughput(dev, cpu=not args.no_cpu_baseline),
                                   "frame_crops": crop_throughput(dev), "inference_b1": inference_latency(dev)}
     if rank == 0 and not args.no_cpu_baseline:
@@ -327,8 +331,9 @@ def _time_fn(fn, reps):
 
 def rgb_fp32_forward(dev, B=32, reps=10):
     """BASELINE configs[1]: PoseNetRGB bs32 224^2, fp32 (reference numerics), forward
-    of the drop-in module (eval mode, no autograd) -> crops/s and the HBM fraction
-    of SURVEY.md §8d's fp32 fused-ideal forward bytes."""
+    of the drop-in module (eval mode, no autograd) -> crops/s.  The fp32 forward is
+    compute-bound (70 flop/B > the 19.7 flop/B fp32 ridge), so the
+    roofline is the fp32 MFMA peak; the HBM fraction is kept beside it."""
     from models.pose_net_rgb import PoseNetRGB
     torch.manual_seed(0)
     m = PoseNetRGB(pretrained=False).to(dev).set_compute_dtype(torch.float32).eval()
@@ -336,10 +341,47 @@ def rgb_fp32_forward(dev, B=32, reps=10):
     with torch.no_grad():
         t = _time_fn(lambda: m(x), reps)
     gbs = FWD_BYTES_PER_CROP_F32 * B / t / 1e9
+    tf = RGB_FWD_FLOPS_PER_CROP * B / t / 1e12
     return {"workload": "PoseNetRGB forward, eval mode, bs32 224^2, fp32", "value": round(B / t, 1),
             "unit": "crops/s", "ms_per_batch": round(t * 1e3, 4), "dtype": "f32",
+            "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tf / PEAK_F32_MFMA_TFLOPS, 4),
+                         "algorithmic_flops_per_crop": RGB_FWD_FLOPS_PER_CROP},
             "hbm_roofline": {"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_bytes_per_crop": FWD_BYTES_PER_CROP_F32}}
+
+
+def dropin_fp32_train(dev, B=32, steps=5):
+    """The path unchanged reference scripts run (train_rgbd_geometric.py:97-115): the
+    drop-in PoseNetRGBDGeometric in its default fp32, driven by autograd, PoseLoss(1,
+    10, geodesic), torch's clip_grad_norm_(1.0) and torch.optim.AdamW -- crops/s."""
+    from models.pose_loss import PoseLoss
+    from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
+    torch.manual_seed(0)
+    model = PoseNetRGBDGeometric(pretrained=False).to(dev).train()
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
+    crit = PoseLoss(rot_weight=1.0, trans_weight=10.0, rotation_loss="geodesic")
+    rgb, depth_raw, bbox, K, gr, gt = synth_batch(B, dev, seed=7)
+
+    def one():
+        opt.zero_grad()
+        rot, trans = model(rgb, None, depth_raw, bbox, K)
+        loss = crit(rot, trans, gr, gt)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        return loss
+    for _ in range(2):
+        one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    return {"workload": "drop-in PoseNetRGBDGeometric fp32 train step through autograd + torch clip_grad_norm_ + "
+                        "torch AdamW (train_rgbd_geometric.py:106-112 unchanged), bs32 224^2",
+            "value": round(B / dt, 1), "unit": "crops/s", "ms_per_step": round(dt * 1e3, 3), "dtype": "f32"}
 
 
 def add_eval_throughput(dev, B=256, N=2000, reps=10, cpu=True):

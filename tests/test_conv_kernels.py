@@ -147,7 +147,7 @@ def test_conv_fast_variants_bit_identical(cfg, monkeypatch):
         return y.cpu(), dx.cpu(), dw.cpu()
 
     y0, dx0, dw0 = run()
-    variants = [{"POSE6D_CONV_STAGES": str(st), "POSE6D_CONV_TILE": str(t)} for st in (2, 3, 4, 6) for t in (0, 1, 3)]
+    variants = [{"POSE6D_CONV_STAGES": str(st), "POSE6D_CONV_TILE": str(t)} for st in (2, 3, 4, 6) for t in (0, 1, 3, 4, 5)]
     variants.append({"POSE6D_CONV_S2": "0"})
     variants += [{"POSE6D_WGRAD_STAGES": str(st)} for st in (2, 3, 4)]
     keys = ("POSE6D_CONV_STAGES", "POSE6D_CONV_TILE", "POSE6D_CONV_S2", "POSE6D_WGRAD_STAGES")

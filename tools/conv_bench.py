@@ -48,8 +48,10 @@ def main():
     ap.add_argument("--env", default="", help="';'-separated K=V[,K=V] settings to sweep for fwd / dgrad")
     ap.add_argument("--B", type=int, default=32)
     ap.add_argument("--only", default="", help="comma-separated indices into SHAPES")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     a = ap.parse_args()
-    B, dt, dtype, dev = a.B, DTYPES[torch.bfloat16], torch.bfloat16, "cuda"
+    dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    B, dt, dev = a.B, DTYPES[dtype], "cuda"
     st = stream()
     tot = {}
     for (H, W, Cin, Cout, k, s, p) in (SHAPES if not a.only else [SHAPES[int(i)] for i in a.only.split(",")]):

@@ -10,5 +10,6 @@ cd $GRAFT_REPO_ROOT
 CSV=$(ls $OUT/*/run_kernel_trace.csv $OUT/run_kernel_trace.csv 2>/dev/null | head -1)
 python3 tools/trace_window.py $CSV --steps 10 --top 60 > $OUT/window.txt 2>&1
 python3 tools/trace_layers.py $CSV > $OUT/layers.txt 2>&1
+python3 tools/trace_seq.py $CSV > $OUT/seq.txt 2>&1
 rm -f $CSV
 exit 0
