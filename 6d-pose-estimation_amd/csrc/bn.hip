@@ -116,6 +116,15 @@ __global__ __launch_bounds__(kThreads) void bn_stats_finalize_kernel(
   const int lane = threadIdx.x % L;
   const int c = blockIdx.x * (kThreads / L) + threadIdx.x / L;
   double s1 = 0.0, s2 = 0.0, K = 0.0;
+  // the per-channel parameters and running statistics the tail needs, fetched now
+  // so their round trip overlaps the partial-row reduction instead of following it
+  float g_c = 0.f, b_c = 0.f, rm_c = 0.f, rv_c = 0.f;
+  if (lane == 0 && c < C) {
+    g_c = gamma[c];
+    b_c = beta[c];
+    rm_c = rmean[c];
+    rv_c = rvar[c];
+  }
   if (c < C) {
     const float* ps = part + (int64_t)c * rows;          // channel-major partials: coalesced rows
     const float* pq = part + ((int64_t)C + c) * rows;
@@ -165,14 +174,14 @@ __global__ __launch_bounds__(kThreads) void bn_stats_finalize_kernel(
     double var = (s2 - s1 * s1 / N) / N;
     if (var < 0.0) var = 0.0;
     const float inv = (float)(1.0 / sqrt(var + (double)eps));
-    const float sc = gamma[c] * inv;
+    const float sc = g_c * inv;
     scale[c] = sc;
-    shift[c] = beta[c] - (float)mean * sc;
+    shift[c] = b_c - (float)mean * sc;
     smean[c] = (float)mean;
     sinv[c] = inv;
     const double unb = N > 1.0 ? var * N / (N - 1.0) : var;
-    rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
-    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+    rmean[c] = (1.f - momentum) * rm_c + momentum * (float)mean;
+    rvar[c] = (1.f - momentum) * rv_c + momentum * (float)unb;
     if (c == 0 && nbt) nbt[0] += 1;
   }
 }
@@ -416,6 +425,16 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_finalize_kernel(const float* 
   if (c >= C) return;
   const float* ps = part + (int64_t)c * rows;
   const float* pq = part + ((int64_t)C + c) * rows;
+  // the tail's operands, fetched before the reduction (their round trip overlaps it)
+  float g_c = 0.f, i_c = 0.f, db0 = 0.f, dg0 = 0.f;
+  if (lane == 0) {
+    g_c = gamma[c];
+    i_c = inv[c];
+    if (accumulate) {
+      if (dbeta) db0 = dbeta[c];
+      if (dgamma) dg0 = dgamma[c];
+    }
+  }
   double s = 0.0, q = 0.0;
   int r = lane;
   for (; r + 64 < rows; r += 128) {
@@ -430,9 +449,9 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_finalize_kernel(const float* 
   s = p6::wave_sum(s);
   q = p6::wave_sum(q);
   if (lane == 0) {
-    if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)s;
-    if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + (float)q;
-    coef[c] = gamma[c] * inv[c];            // c1
+    if (dbeta) dbeta[c] = db0 + (float)s;
+    if (dgamma) dgamma[c] = dg0 + (float)q;
+    coef[c] = g_c * i_c;                    // c1
     coef[C + c] = (float)(s / count);       // c2 = mean(dz)
     coef[2 * C + c] = (float)(q / count);   // c3 = mean(dz * xhat)
   }

@@ -855,7 +855,8 @@ __global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const bf16* __restri
   if (b < nd_pad) {
     if (b < nd) conv_lds_body<bf16, 64, 64, DMODE, DS, BNF>(smem, b, dy, wt, nullptr, dres, dx, nullptr, gd, &bn);
   } else if (b < nd_pad + nw) {
-    conv_wgrad_lds_body<64, 64, WS>(smem, b - nd_pad, x, dy, ws, gw);
+    // kGemm data gradient <=> pointwise conv: the weight gradient takes the pointwise body
+    conv_wgrad_lds_body<64, 64, WS, DMODE == kGemm>(smem, b - nd_pad, x, dy, ws, gw);
   } else {
     // the previous conv's weight-gradient slabs (another workspace), reduced here
     // instead of in a launch of their own

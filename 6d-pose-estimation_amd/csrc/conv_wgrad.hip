@@ -240,12 +240,12 @@ int launch_reduce(const float* ws, float* dw, int Cout, int Kpad, int SC, int Ci
 
 using Plan = p6::WgradPlan;
 
-template <int S>
+template <int S, bool PW>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_lds_kernel(const bf16* __restrict__ x,
                                                                   const bf16* __restrict__ dy,
                                                                   float* __restrict__ ws, WGeom g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv_wgrad_lds_body<64, 64, S>(smem, blockIdx.x, x, dy, ws, g);
+  conv_wgrad_lds_body<64, 64, S, PW>(smem, blockIdx.x, x, dy, ws, g);
 }
 
 int env_int(const char* name, int dflt) {
@@ -305,7 +305,12 @@ template <int S>
 int launch_fast(const WGeom& g, const void* x, const void* dy, float* ws, hipStream_t s) {
   static_assert(S * (64 + 64) * 128 >= acc_stage_bytes<64, 64>(), "ring too small to stage the tile");
   const int lds = S * (64 + 64) * 128;
-  conv_wgrad_lds_kernel<S><<<g.gm * g.gn * g.splits, kThreads, lds, s>>>((const bf16*)x, (const bf16*)dy, ws, g);
+  if (g.KH == 1 && g.KW == 1 && g.stride == 1 && g.pad == 0)
+    conv_wgrad_lds_kernel<S, true><<<g.gm * g.gn * g.splits, kThreads, lds, s>>>((const bf16*)x, (const bf16*)dy, ws,
+                                                                                 g);
+  else
+    conv_wgrad_lds_kernel<S, false><<<g.gm * g.gn * g.splits, kThreads, lds, s>>>((const bf16*)x, (const bf16*)dy,
+                                                                                  ws, g);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }

@@ -120,7 +120,13 @@ __device__ __forceinline__ void lds_wait_tr8(u32x2 (&f)[8]) {
 // one workgroup's work; `bid` = its index in the weight-gradient sub-grid (whose
 // size is a multiple of 8 or the whole grid, so bid & 7 is its XCD), `smem` = the
 // kernel's dynamic LDS
-template <int BM, int BN, int S>
+// PW: pointwise conv (1x1, stride 1, no padding) -- X rows are the output pixels
+// themselves, so every operand row advances by a constant stride per 64-pixel stage
+// and only the split's last stage can run past its end: the per-stage issue is a
+// pointer increment and one compare per row instead of the general (n, oy, ox)
+// walk with per-row padding checks (which left the 1x1 weight gradients issue
+// bound: ~1200 issue cycles per wave per K-step against 128 of MFMA)
+template <int BM, int BN, int S, bool PW = false>
 __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const bf16* __restrict__ x,
                                                     const bf16* __restrict__ dy, float* __restrict__ ws,
                                                     const p6::WGeom& g) {
@@ -148,7 +154,7 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
   const int wm = wave >> 1, wn = wave & 1;
   const int r8 = lane >> 3, pch = lane & 7;
   const char* zp = reinterpret_cast<const char*>(g_zero_page);
-  const bool pointwise = g.KH == 1 && g.KW == 1 && g.stride == 1 && g.pad == 0;
+  constexpr bool pointwise = PW;
 
   // each thread DMAs rows R = i * 32 + wave * 8 + r8 (i = 0, 1) of every sub-image;
   // the logical chunk it fetches carries the row's swizzle
@@ -180,8 +186,44 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
     }
   }
 
+  // pointwise: per-row operand pointers advanced by a stage each issue
+  const bf16* pw_y[2][YS];
+  const bf16* pw_x[2][XS];
+  int pw_m[2];
+  if constexpr (PW) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = mbeg + i * 32 + wave * 8 + r8;
+      pw_m[i] = m;
+#pragma unroll
+      for (int s_ = 0; s_ < YS; ++s_) pw_y[i][s_] = dy + (int64_t)m * g.Cout + co0 + s_ * 64 + ck[i];
+#pragma unroll
+      for (int s_ = 0; s_ < XS; ++s_) pw_x[i][s_] = x + ((int64_t)m << g.log2SC) + ci0[s_] + ck[i];
+    }
+  }
+  const int64_t y_step = (int64_t)MS * g.Cout, x_step = (int64_t)MS << g.log2SC;
+
   auto issue = [&](int st, int buf) {
     char* base = smem + buf * STAGE;
+    if constexpr (PW) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool ok = pw_m[i] < mend;
+#pragma unroll
+        for (int s_ = 0; s_ < YS; ++s_)
+          glds16(ok ? (const void*)pw_y[i][s_] : (const void*)zp, base + s_ * SUB + (i * 32 + wave * 8) * 128);
+#pragma unroll
+        for (int s_ = 0; s_ < XS; ++s_)
+          glds16(ok ? (const void*)pw_x[i][s_] : (const void*)zp, base + (YS + s_) * SUB + (i * 32 + wave * 8) * 128);
+        pw_m[i] += MS;
+#pragma unroll
+        for (int s_ = 0; s_ < YS; ++s_) pw_y[i][s_] += y_step;
+#pragma unroll
+        for (int s_ = 0; s_ < XS; ++s_) pw_x[i][s_] += x_step;
+      }
+      (void)st;
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int R = i * 32 + wave * 8 + r8;
