@@ -8,7 +8,10 @@
 //                          clip coefficient min(1, max_norm/(norm+1e-6)); AdamW
 //                          update in torch's operation order.
 // Hyper-parameters come from a device array (graph replays pick up lr changes):
-//   hp = {lr, beta1, beta2, eps, weight_decay, step (t >= 1), unused, max_norm}
+//   hp = {lr, beta1, beta2, eps, weight_decay, step (t >= 1), grad scale, max_norm}
+// grad scale (0 reads as 1) multiplies the gradient before clipping: the DDP trainer
+// sets 1/world so the summed all-reduce result is averaged here instead of in a pass
+// of its own (exact for power-of-two world sizes: the norm scales by the same 2^-k).
 #include "common.h"
 
 namespace {
@@ -47,6 +50,7 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float* __restrict__ p, 
   __shared__ float s_coef;
   __shared__ double red[kThreads / 64];
   const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4], max_norm = hp[7];
+  const float gs = hp[6] != 0.f ? hp[6] : 1.f;
   // bias corrections from the device step counter hp[5] (incremented in-stream, so
   // a captured step replays with the right t): 1 - beta^t as torch computes it
   const double t = (double)hp[5];
@@ -58,7 +62,7 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float* __restrict__ p, 
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
     if (threadIdx.x == 0) {
-      const float norm = (float)sqrt(red[0] + red[1] + red[2] + red[3]);
+      const float norm = gs * (float)sqrt(red[0] + red[1] + red[2] + red[3]);
       const float c = max_norm / (norm + 1e-6f);
       s_coef = c < 1.f ? c : 1.f;
       if (blockIdx.x == 0 && norm_out) norm_out[0] = norm;
@@ -67,8 +71,9 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float* __restrict__ p, 
   } else if (threadIdx.x == 0) {
     s_coef = 1.f;
   }
+  // (the clip coefficient applies to the scaled gradient; fold both into one factor)
   __syncthreads();
-  const float coef = s_coef;
+  const float coef = s_coef * gs;
   const float step_size = lr / bc1;
   const float bc2s = sqrtf(bc2);
   const float decay = 1.f - lr * wd;

@@ -87,8 +87,10 @@ class RGBDGeometricTrainer:
         self.arena = FlatArena(order, dev)
         self.m = torch.zeros_like(self.arena.flat)
         self.v = torch.zeros_like(self.arena.flat)
-        self.hp = torch.tensor([lr, betas[0], betas[1], eps, weight_decay, 0.0, 0.0, max_norm], device=dev,
-                               dtype=torch.float32)
+        self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        # hp[6]: gradient scale read by adamw_step -- 1/world averages the all-reduced sum
+        self.hp = torch.tensor([lr, betas[0], betas[1], eps, weight_decay, 0.0, 1.0 / self.world, max_norm],
+                               device=dev, dtype=torch.float32)
         self.partials = torch.zeros(NPART, device=dev)
         self.norm = torch.zeros(1, device=dev)
         self.loss = torch.zeros((), device=dev)
@@ -101,7 +103,6 @@ class RGBDGeometricTrainer:
         self.seed = torch.tensor([torch.initial_seed() & 0x7FFFFFFFFFFF], device=dev, dtype=torch.int64)
         self.wr, self.wt = float(rot_weight), float(trans_weight)
         self.pg = process_group
-        self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
         self.graphs = None
         self._buckets(bucket_mb)
 
@@ -134,8 +135,8 @@ class RGBDGeometricTrainer:
 
     def _optimizer(self):
         st = stream()
-        if self.world > 1:
-            self.arena.grad.mul_(1.0 / self.world)
+        # (world > 1: the 1/world average of the all-reduced gradient is hp[6], applied
+        # inside adamw_step; the norm partials see the sum, scaled there too)
         # step counter hp[5] += 1 and dropout seed += 1 ride on the norm-partials launch
         # (the seed is next read by the following step's forward)
         call("sumsq_partial_step", self.arena.grad, self.arena.numel, self.partials, NPART,

@@ -403,7 +403,8 @@ int pose6d_xattn_bwd(const float *dout, const float *q, const float *k, const fl
  * Optimiser — clip_grad_norm_(params, max_norm) + AdamW.step() of the callers
  * (train_rgbd_geometric.py:65,111-112) over one flat fp32 buffer.
  * hp (device) = {lr, beta1, beta2, eps, weight_decay, step t (>= 1; bias
- *                corrections 1 - beta^t computed in-kernel), unused,
+ *                corrections 1 - beta^t computed in-kernel), grad scale (applied to
+ *                grad before the norm; 0 reads as 1 — the DDP trainer's 1/world),
  *                max_norm (<= 0: no clipping)}
  * ---------------------------------------------------------------------- */
 int pose6d_sumsq_partial(const float *g, int64_t n, float *partials, int32_t nparts, void *stream);
