@@ -10,6 +10,7 @@ import torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "6d-pose-estimation_amd")]
 
+import pose6d._lib as _plib  # noqa: E402
 from pose6d._lib import call, query, stream  # noqa: E402
 from pose6d.trunk import DTYPES, pack_single  # noqa: E402
 
@@ -26,8 +27,26 @@ SHAPES = [
 ]
 
 
+GRAPH = False
+
+
 def timeit(fn, reps=20):
     fn()
+    if GRAPH:   # the calls replayed from one hipGraph: no host-issue floor (~6 us per ctypes call)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            g.replay()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / (5 * reps) * 1e-3
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
@@ -49,7 +68,13 @@ def main():
     ap.add_argument("--B", type=int, default=32)
     ap.add_argument("--only", default="", help="comma-separated indices into SHAPES")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--lib", default="", help="load this libpose6d build instead (tools/conv_exp.sh variants)")
+    ap.add_argument("--graph", action="store_true", help="time replays of a captured graph (GPU time, no host floor)")
     a = ap.parse_args()
+    global GRAPH
+    GRAPH = a.graph
+    if a.lib:
+        _plib.LIB_PATH = os.path.abspath(a.lib)
     dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     B, dt, dev = a.B, DTYPES[dtype], "cuda"
     st = stream()
@@ -69,15 +94,15 @@ def main():
         dw = torch.empty(Cout, Cin, k, k, device=dev)
         flops = 2.0 * B * Ho * Wo * Cout * Cin * k * k
         fns = {
-            "fwd": lambda: call("conv2d_fwd", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, st),
-            "dgrad": lambda: call("conv2d_dgrad", dt, dy, wt, None, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, st),
-            "dgradip": lambda: call("conv2d_dgrad", dt, dy, wt, dx, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, st),
+            "fwd": lambda: call("conv2d_fwd", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream()),
+            "dgrad": lambda: call("conv2d_dgrad", dt, dy, wt, None, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream()),
+            "dgradip": lambda: call("conv2d_dgrad", dt, dy, wt, dx, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream()),
             "bwdip": lambda: call("conv2d_backward", dt, x, dy, wt, dx, dx, dw, 0, ws, ws.numel() * 4, B, H, W, Cin,
-                                  Cin, Cout, k, k, s, p, Ho, Wo, st),
+                                  Cin, Cout, k, k, s, p, Ho, Wo, stream()),
             "bwd": lambda: call("conv2d_backward", dt, x, dy, wt, None, dx, dw, 0, ws, ws.numel() * 4, B, H, W, Cin,
-                                Cin, Cout, k, k, s, p, Ho, Wo, st),
+                                Cin, Cout, k, k, s, p, Ho, Wo, stream()),
             "wgrad": lambda: call("conv2d_wgrad", dt, x, dy, dw, 0, ws, ws.numel() * 4, B, H, W, Cin, Cin, Cout, k, k,
-                                  s, p, Ho, Wo, st),
+                                  s, p, Ho, Wo, stream()),
         }
         line = f"{H:3d}x{W:<3d} {Cin:4d}->{Cout:<4d} k{k}s{s} |"
         for ps in a.passes.split(","):
