@@ -50,6 +50,10 @@ struct Geom {
   // (pose6d_conv2d_fwd_act); `res` is then the residual tensor
   const float *act_scale, *act_shift, *act_rscale, *act_rshift;
   int act, act_relu;
+  // data gradient: the residual contribution is res * mask (one bit per element, one
+  // byte per 16-byte chunk: pose6d_bn_act_fwd_mask's ReLU bits), i.e. the masked dout
+  // of the block's last BN, instead of a materialised dz (null = res as is)
+  const uint8_t* res_mask;
 };
 
 // kDgradS2 launched in place (dres == dx) when a single parity class has taps
@@ -256,11 +260,13 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / (16 * (NW / 2))]
       __builtin_memcpy(&v, a, 16);
     } else if (res) {
       const uint4 rv = *reinterpret_cast<const uint4*>(res + om * g.Ncols + c);
+      const unsigned mb = g.res_mask ? (unsigned)g.res_mask[(om * g.Ncols + c) / E] : 0xFFu;
       T a[E], b[E];
       __builtin_memcpy(a, &v, 16);
       __builtin_memcpy(b, &rv, 16);
 #pragma unroll
-      for (int e = 0; e < E; ++e) a[e] = p6::from_f<T>(p6::to_f(a[e]) + p6::to_f(b[e]));
+      for (int e = 0; e < E; ++e)
+        a[e] = p6::from_f<T>(p6::to_f(a[e]) + ((mb >> e) & 1u ? p6::to_f(b[e]) : 0.f));
       __builtin_memcpy(&v, a, 16);
     }
     *reinterpret_cast<uint4*>(dst) = v;
@@ -1189,17 +1195,27 @@ extern "C" int pose6d_conv2d_fwd_act(int32_t dtype, const void* x, const void* w
   return run_conv(dtype, mode, g, x, w, bias, res, out, nullptr, p6::stream_of(stream));
 }
 
-extern "C" int pose6d_conv2d_dgrad(int32_t dtype, const void* dy, const void* wt, const void* dres, void* dx,
-                                   int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW,
-                                   int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, void* stream) {
+namespace {
+int dgrad_impl(int32_t dtype, const void* dy, const void* wt, const void* dres, const uint8_t* dres_mask, void* dx,
+               int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
+               int32_t pad, int32_t Ho, int32_t Wo, void* stream) {
   P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_dgrad: bad dtype %d", dtype);
   P6_CHECK_ARG(stride == 1 || stride == 2, "pose6d_conv2d_dgrad: stride must be 1 or 2");
   P6_CHECK_ARG(Cin % 8 == 0, "pose6d_conv2d_dgrad: Cin %% 8 != 0 (no data gradient for the stem)");
+  P6_CHECK_ARG(!dres_mask || (dres && dres != dx), "pose6d_conv2d_dgrad: a residual mask needs a separate dres");
   const int bk = dtype == POSE6D_DT_BF16 ? 32 : 16;
   int mode;
-  const Geom g = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
+  Geom g = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
+  g.res_mask = dres_mask;
   P6_CHECK_ARG(g.log2SC >= 0 && Cout % bk == 0, "pose6d_conv2d_dgrad: Cout must be a power of two >= %d", bk);
   return run_conv(dtype, mode, g, dy, wt, nullptr, dres, dx, nullptr, p6::stream_of(stream));
+}
+}  // namespace
+
+extern "C" int pose6d_conv2d_dgrad(int32_t dtype, const void* dy, const void* wt, const void* dres, void* dx,
+                                   int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW,
+                                   int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, void* stream) {
+  return dgrad_impl(dtype, dy, wt, dres, nullptr, dx, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, stream);
 }
 
 namespace {
@@ -1267,7 +1283,8 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
                        float* dw, int32_t accumulate, float* workspace, int64_t ws_bytes, int32_t N, int32_t H,
                        int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
                        int32_t pad, int32_t Ho, int32_t Wo, int32_t phases, const BnBwd& bn, void* stream,
-                       const ReduceJob* rj = nullptr, int32_t* deferred = nullptr);
+                       const ReduceJob* rj = nullptr, int32_t* deferred = nullptr,
+                       const uint8_t* dres_mask = nullptr);
 }  // namespace
 
 extern "C" int pose6d_conv2d_backward_ex(int32_t dtype, const void* x, const void* dy, const void* wt,
@@ -1318,7 +1335,7 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
                        float* dw, int32_t accumulate, float* workspace, int64_t ws_bytes, int32_t N, int32_t H,
                        int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
                        int32_t pad, int32_t Ho, int32_t Wo, int32_t phases, const BnBwd& bn, void* stream,
-                       const ReduceJob* rj, int32_t* deferred) {
+                       const ReduceJob* rj, int32_t* deferred, const uint8_t* dres_mask) {
   P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_backward: bad dtype %d", dtype);
   if (deferred) *deferred = 0;
   const ReduceJob none{};
@@ -1338,8 +1355,11 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
   P6_CHECK_ARG(stride == 1 || stride == 2, "pose6d_conv2d_backward: stride must be 1 or 2");
   P6_CHECK_ARG(Cin % 8 == 0 && Cin_real <= Cin && ilog2(Cin) >= 3,
                "pose6d_conv2d_backward: Cin must be a power of two >= 8 for the data gradient");
+  P6_CHECK_ARG(!dres_mask || (dres && dres != dx && !bn.part),
+               "pose6d_conv2d_backward: a residual mask needs a separate dres (and no BN epilogue)");
   int mode;
-  const Geom gd0 = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
+  Geom gd0 = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
+  gd0.res_mask = dres_mask;
   const Plan pd = choose(dtype, mode, gd0, true);
   p6::WgradPlan pw;
   const p6::WGeom gw = p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
@@ -1348,7 +1368,7 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
     if (!(phases & 1)) return POSE6D_OK;
     int rc = flush_prev();
     if (rc) return rc;
-    rc = pose6d_conv2d_dgrad(dtype, dy, wt, dres, dx, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, stream);
+    rc = dgrad_impl(dtype, dy, wt, dres, dres_mask, dx, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, stream);
     if (rc) return rc;
     return pose6d_conv2d_wgrad(dtype, x, dy, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real, Cout, KH,
                                KW, stride, pad, Ho, Wo, stream);
@@ -1442,4 +1462,23 @@ extern "C" int pose6d_conv2d_backward_chain(int32_t dtype, const void* x, const 
   }
   return conv_backward_impl(dtype, x, dy, wt, dres, dx, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real,
                             Cout, KH, KW, stride, pad, Ho, Wo, 3, BnBwd{}, stream, prev ? &r : nullptr, deferred);
+}
+
+extern "C" int pose6d_conv2d_backward_chain_masked(int32_t dtype, const void* x, const void* dy, const void* wt,
+                                                   const void* dres, const uint8_t* dres_mask, void* dx, float* dw,
+                                                   int32_t accumulate, float* workspace, int64_t ws_bytes, int32_t N,
+                                                   int32_t H, int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout,
+                                                   int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho,
+                                                   int32_t Wo, const pose6d_wgrad_reduce_t* prev, int32_t* deferred,
+                                                   void* stream) {
+  P6_CHECK_ARG(deferred != nullptr, "pose6d_conv2d_backward_chain_masked: deferred must point to an int32");
+  P6_CHECK_ARG(dres_mask != nullptr, "pose6d_conv2d_backward_chain_masked: null mask");
+  ReduceJob r{};
+  if (prev) {
+    P6_CHECK_ARG(prev->ws != workspace, "pose6d_conv2d_backward_chain: prev slabs must live in another workspace");
+    r = make_job(*prev);
+  }
+  return conv_backward_impl(dtype, x, dy, wt, dres, dx, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real,
+                            Cout, KH, KW, stride, pad, Ho, Wo, 3, BnBwd{}, stream, prev ? &r : nullptr, deferred,
+                            dres_mask);
 }

@@ -218,11 +218,15 @@ class TrunkEngine:
                                        op.k))
                 ws_bn = max(ws_bn, (query("bn_bwd_workspace_rows", M) * 2 + 3) * op.cout)
             elif isinstance(op, _ActOp):
-                op.dz = e(B, o.H, o.W, o.C) if (op.res_act is not None or op.res_conv is not None) else None
-                # residual BN + ReLU: one mask bit per element replaces re-reading `out` in backward
+                residual = op.res_act is not None or op.res_conv is not None
+                # residual BN + ReLU: one mask bit per element replaces re-reading `out` in
+                # backward, and the identity branch's gradient dz = dout * mask is never
+                # written out: its consumers (the next block's conv1 data gradient, the
+                # downsample BN's backward) apply the bits to dout themselves
                 vec = 8 if dtype == torch.bfloat16 else 4
                 op.mbits = (torch.empty(B * o.H * o.W * o.C // vec, device=device, dtype=torch.uint8)
-                            if (op.relu and op.dz is not None) else None)
+                            if (op.relu and residual) else None)
+                op.dz = e(B, o.H, o.W, o.C) if (residual and op.mbits is None) else None
             elif isinstance(op, _PoolOp):
                 op.argmax = torch.empty(B, o.H, o.W, o.C, device=device, dtype=torch.uint8)
         self.ws_wgrad = f32(max(ws_w // 4, 1))
@@ -423,21 +427,30 @@ class TrunkEngine:
                 if op.res_conv is not None:
                     r = op.res_conv
                     # identity branch = bn_r(y_r) (no ReLU of its own): its dz is the masked dout
-                    call("bn_bwd", dt, op.dz, None, None, None, r.out.t, r.mean, r.inv, r.bn.weight.detach(),
-                         grad_of(r.bn.weight), grad_of(r.bn.bias), acc, r.out.g, None, self.ws_bn, M, r.cout, st)
+                    if op.mbits is not None:
+                        call("bn_bwd_mask", dt, op.out.g, op.mbits, r.out.t, r.mean, r.inv, r.bn.weight.detach(),
+                             grad_of(r.bn.weight), grad_of(r.bn.bias), acc, r.out.g, None, self.ws_bn, M, r.cout,
+                             st)
+                    else:
+                        call("bn_bwd", dt, op.dz, None, None, None, r.out.t, r.mean, r.inv, r.bn.weight.detach(),
+                             grad_of(r.bn.weight), grad_of(r.bn.bias), acc, r.out.g, None, self.ws_bn, M, r.cout, st)
                 elif op.res_act is not None:
-                    op.res_act.pending = op.dz
+                    # the identity gradient: dz itself, or (dout, mask bits) applied by the consumer
+                    op.res_act.pending = op.dz if op.mbits is None else (op.out.g, op.mbits)
             elif isinstance(op, _ConvOp):
                 dy = op.out.g
                 M = B * op.Ho * op.Wo
-                dres, dx = None, None
+                dres, dx, dmask = None, None, None
                 final = True   # dx is the complete gradient of op.src
                 if op.needs_dgrad:
                     src = op.src
                     if src.pending is not None and src.g is not None:
                         # a contribution is waiting: fuse it into this dgrad's epilogue (in
-                        # place when it already sits in src.g: dres == dx)
+                        # place when it already sits in src.g: dres == dx; as dout * mask
+                        # bits when it is a residual BN's masked output gradient)
                         dres, dx = src.pending, src.g
+                        if isinstance(dres, tuple):
+                            dres, dmask = dres
                         src.pending = None
                     elif src.pending is None and self._has_later_consumer(op):
                         # first of two contributions (conv1; the downsample conv adds to it)
@@ -454,7 +467,7 @@ class TrunkEngine:
                 args = (dt, op.src.t, dy, op.wt, dres, dx, dw, acc, ws, ws.numel() * 4, B, op.H, op.W, op.cin_pad,
                         op.cin, op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo)
                 a = op.bn_act
-                if a is not None and op.bn_rows > 0 and final and dx is op.src.g and dres is not dx:
+                if a is not None and op.bn_rows > 0 and final and dx is op.src.g and dres is not dx and dmask is None:
                     # dx is the final dout of BN `a`: its partial sums come out of this epilogue
                     if pending is not None:
                         call("wgrad_reduce", ctypes.addressof(pending), st)
@@ -471,8 +484,12 @@ class TrunkEngine:
                 else:
                     job = _WgradReduce(ws.data_ptr(), dw.data_ptr(), dt, B, op.H, op.W, op.cin_pad, op.cin, op.cout,
                                        op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, acc)
-                    call("conv2d_backward_chain", *args, ctypes.addressof(pending) if pending is not None else None,
-                         ctypes.addressof(deferred), st)
+                    prev = ctypes.addressof(pending) if pending is not None else None
+                    if dmask is not None:
+                        call("conv2d_backward_chain_masked", dt, op.src.t, dy, op.wt, dres, dmask, *args[5:], prev,
+                             ctypes.addressof(deferred), st)
+                    else:
+                        call("conv2d_backward_chain", *args, prev, ctypes.addressof(deferred), st)
                     if pending_op is not None:
                         conv_done(pending_op)          # its reduce ran in this launch (or just before it)
                     if deferred.value:

@@ -250,6 +250,16 @@ int pose6d_conv2d_backward_chain(int32_t dtype, const void *x, const void *dy, c
                                  int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout,
                                  int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
                                  const pose6d_wgrad_reduce_t *prev, int32_t *deferred, void *stream);
+/* pose6d_conv2d_backward_chain whose residual contribution is dres * mask instead of
+ * dres: dres_mask = pose6d_bn_act_fwd_mask's ReLU bits for dres (bit e of byte i masks
+ * element i * E + e, E = 8 bf16 / 4 fp32), i.e. dres = the block output's gradient and
+ * the product = the dz a residual BN backward would otherwise write out; dres != dx. */
+int pose6d_conv2d_backward_chain_masked(int32_t dtype, const void *x, const void *dy, const void *wt,
+                                        const void *dres, const uint8_t *dres_mask, void *dx, float *dw,
+                                        int32_t accumulate, float *workspace, int64_t ws_bytes, int32_t N, int32_t H,
+                                        int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH,
+                                        int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
+                                        const pose6d_wgrad_reduce_t *prev, int32_t *deferred, void *stream);
 /* (1 << 16) | (data-gradient mode << 4) | ring stages when pose6d_conv2d_backward
  * runs ONE fused conv_bwd_kernel<mode, stages, 3> launch (+ the reduce), else 0 */
 int pose6d_bwd_variant(int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH,

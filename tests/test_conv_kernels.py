@@ -283,6 +283,58 @@ def test_bn_act_and_backward(dtype, C, N, H):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cfg", [(4, 14, 14, 256, 64, 1, 1, 0), (2, 14, 14, 64, 64, 3, 1, 1)])
+def test_backward_masked_residual(cfg, dtype):
+    """conv backward whose residual is (dout, ReLU bits) equals the one fed the
+    materialised dz = dout * mask (the residual BN backward's dz_out), bit for bit,
+    dW included; the bits are pose6d_bn_act_fwd_mask's."""
+    import ctypes
+    from pose6d._lib import call, query, stream
+    from pose6d.trunk import DTYPES, pack_single
+    N, H, W, Cin, Cout, k, s, p = cfg
+    g = torch.Generator().manual_seed(11)
+    dev, dt = "cuda", DTYPES[dtype]
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    M = N * H * W
+    x = _nhwc(torch.randn(N, Cin, H, W, generator=g)).to(dev, dtype)
+    w = (torch.randn(Cout, Cin, k, k, generator=g) * 0.05).to(dev)
+    _, wt = pack_single(w, Cin, dtype)
+    dy = _nhwc(torch.randn(N, Cout, Ho, Wo, generator=g)).to(dev, dtype)
+    # the residual BN's forward: out = relu(y * sc + sh + res), bits = out > 0
+    yraw = _nhwc(torch.randn(N, Cin, H, W, generator=g)).to(dev, dtype)
+    res = _nhwc(torch.randn(N, Cin, H, W, generator=g)).to(dev, dtype)
+    sc = (torch.rand(Cin, generator=g) + 0.5).to(dev)
+    sh = torch.randn(Cin, generator=g).to(dev)
+    out = torch.empty_like(yraw)
+    vec = 8 if dtype == torch.bfloat16 else 4
+    bits = torch.empty(M * Cin // vec, device=dev, dtype=torch.uint8)
+    call("bn_act_fwd_mask", dt, yraw, sc, sh, res, None, None, 1, out, bits, M, Cin, stream())
+    dout = _nhwc(torch.randn(N, Cin, H, W, generator=g)).to(dev, dtype)
+    dz = torch.where(out > 0, dout, torch.zeros_like(dout))
+    ws = torch.empty(query("conv2d_wgrad_workspace", dt, N, Ho, Wo, Cin, Cout, k, k) // 4 + 1, device=dev)
+    res_out = []
+    for masked in (False, True):
+        dx = torch.full_like(x, float("nan"))
+        dw = torch.empty(Cout, Cin, k, k, device=dev)
+        deferred = ctypes.c_int32(0)
+        tail = (dx, dw, 0, ws, ws.numel() * 4, N, H, W, Cin, Cin, Cout, k, k, s, p, Ho, Wo, None,
+                ctypes.addressof(deferred), stream())
+        if masked:
+            call("conv2d_backward_chain_masked", dt, x, dy, wt, dout, bits, *tail)
+        else:
+            call("conv2d_backward_chain", dt, x, dy, wt, dz, *tail)
+        if deferred.value:   # this conv's slab reduce was left for a following launch
+            from pose6d.trunk import _WgradReduce
+            job = _WgradReduce(ws.data_ptr(), dw.data_ptr(), dt, N, H, W, Cin, Cin, Cout, k, k, s, p, Ho, Wo, 0)
+            call("wgrad_reduce", ctypes.addressof(job), stream())
+        torch.cuda.synchronize()
+        res_out.append((dx.clone(), dw.clone()))
+    assert torch.equal(res_out[0][0], res_out[1][0]), "masked residual dX differs"
+    assert torch.equal(res_out[0][1], res_out[1][1]), "dW differs"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_pools(dtype):
     from pose6d._lib import call, stream
     from pose6d.trunk import DTYPES
