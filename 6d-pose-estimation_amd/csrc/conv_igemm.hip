@@ -1106,8 +1106,11 @@ Plan choose(int dtype, int mode, const Geom& g, bool fused = false) {
   const bool cols128 = p.tile == 0 || p.tile == 4;
   const int64_t grid = (int64_t)p6::ceil_div(p.g.M, rows128 ? 128 : 64) * p6::ceil_div(g.Ncols, cols128 ? 128 : 64) *
                        (p.mode == kDgradS2 ? 4 : 1);
-  p.stages = env_int("POSE6D_CONV_STAGES",
-                     (fast_nk(p.mode, p.g, dtype == POSE6D_DT_BF16 ? 64 : 32) > 24 && grid <= 512) ? 4 : 2);
+  int dflt = (fast_nk(p.mode, p.g, dtype == POSE6D_DT_BF16 ? 64 : 32) > 24 && grid <= 512) ? 4 : 2;
+  // fp32 forward (MFMA-bound: 4 exact 16x16x4 MFMAs per 16-byte chunk): 3 slots for
+  // 1x1 filters, 2 for the rest (tools/conv_bench.py --graph --dtype f32 sweep, round 2)
+  if (dtype == POSE6D_DT_F32 && (p.mode == kGemm || p.mode == kFwd)) dflt = (g.KH == 1 && g.KW == 1) ? 3 : 2;
+  p.stages = env_int("POSE6D_CONV_STAGES", dflt);
   if (p.stages < 2) p.stages = 2;
   if (p.stages > 6) p.stages = 6;
   if (p.stages == 5) p.stages = 4;
