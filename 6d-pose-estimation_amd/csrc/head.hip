@@ -98,11 +98,9 @@ __global__ __launch_bounds__(kSkThreads) void skinny_gemm_kernel(
   const int kb = w * kc, ke = min(K, kb + kc);
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   const bool m0ok = r < M, m1ok = r + 16 < M, nok = n < N;
-  // KU 16-deep chunks per trip with every operand load issued before the first MFMA
-  // (one chunk per trip left the waves latency bound: ~11 us for a 2048 x 2048 weight
-  // that streams in ~3); the MFMA order per accumulator is unchanged
-  constexpr int KU = 4;
-  auto load = [&](int kq, float (&a0)[4], float (&a1)[4], float (&b)[4]) {
+  for (int k = kb; k < ke; k += 16) {
+    const int kq = k + 4 * q;
+    float a0[4], a1[4], b[4];
     if (VEC && kq + 3 < ke) {
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
       const f32x4 va0 = m0ok ? *reinterpret_cast<const f32x4*>(A + r * sam + kq) : z;
@@ -127,23 +125,6 @@ __global__ __launch_bounds__(kSkThreads) void skinny_gemm_kernel(
         b[s] = (kok && nok) ? (BKC ? B[n * sbn + kk] : B[(int64_t)kk * sbk + n]) : 0.f;
       }
     }
-  };
-  int k = kb;
-  for (; k + 16 * (KU - 1) < ke; k += 16 * KU) {
-    float a0[KU][4], a1[KU][4], b[KU][4];
-#pragma unroll
-    for (int u = 0; u < KU; ++u) load(k + 16 * u + 4 * q, a0[u], a1[u], b[u]);
-#pragma unroll
-    for (int u = 0; u < KU; ++u)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[u][s], b[u][s], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u][s], b[u][s], acc1, 0, 0, 0);
-      }
-  }
-  for (; k < ke; k += 16) {
-    float a0[4], a1[4], b[4];
-    load(k + 4 * q, a0, a1, b);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], b[s], acc0, 0, 0, 0);
