@@ -79,6 +79,7 @@ def main():
     B, dt, dev = a.B, DTYPES[dtype], "cuda"
     st = stream()
     tot = {}
+    flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev) if "fwdcold" in a.passes else None
     for (H, W, Cin, Cout, k, s, p) in (SHAPES if not a.only else [SHAPES[int(i)] for i in a.only.split(",")]):
         Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         x = torch.randn(B, H, W, Cin, device=dev).to(dtype)
@@ -95,6 +96,13 @@ def main():
         flops = 2.0 * B * Ho * Wo * Cout * Cin * k * k
         fns = {
             "fwd": lambda: call("conv2d_fwd", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream()),
+            # no BN statistics (as in eval without the fold)
+            "fwdns": lambda: call("conv2d_fwd", dt, x, wp, None, y, None, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo,
+                                  stream()),
+            # each call behind a 512 MB write (caches hold none of the conv's operands), minus that write's time
+            "fwdcold": lambda: (flush.zero_(), call("conv2d_fwd", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k,
+                                                    k, s, p, Ho, Wo, stream())),
+            "flush": lambda: flush.zero_(),
             "dgrad": lambda: call("conv2d_dgrad", dt, dy, wt, None, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream()),
             "dgradip": lambda: call("conv2d_dgrad", dt, dy, wt, dx, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream()),
             "bwdip": lambda: call("conv2d_backward", dt, x, dy, wt, dx, dx, dw, 0, ws, ws.numel() * 4, B, H, W, Cin,
@@ -105,6 +113,8 @@ def main():
                                   s, p, Ho, Wo, stream()),
         }
         line = f"{H:3d}x{W:<3d} {Cin:4d}->{Cout:<4d} k{k}s{s} |"
+        if "fwdcold" in a.passes.split(","):
+            line += f" flush:{timeit(fns['flush']) * 1e6:6.1f}us"
         for ps in a.passes.split(","):
             if ps in ("dgrad", "bwd", "dgradip", "bwdip") and Cin % 8:
                 continue   # the stem has no data gradient
@@ -137,7 +147,7 @@ def main():
                             line += f" {ps}:{impl}/{t}/{nst}=ERR({str(e)[:120]})"
                             continue
                         tf = flops / sec / 1e12
-                        tag = f"{ps[0]}{impl[0]}{t}" + (f"s{nst}" if impl == "fast" else "")
+                        tag = f"{ps}/{impl[0]}{t}" + (f"s{nst}" if impl == "fast" else "")
                         line += f" {tag}:{sec * 1e6:6.1f}us/{tf:5.0f}T"
                         if t == "auto" and nst == "auto":
                             tot[(ps, impl)] = tot.get((ps, impl), 0.0) + sec
