@@ -11,7 +11,8 @@ import re
 import torch  # noqa: F401  (loads torch's HIP runtime first; libpose6d binds to the same libamdhip64.so.7)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libpose6d.so")
+# POSE6D_LIB: another build of the same library (A/B timing of two builds on one box)
+LIB_PATH = os.environ.get("POSE6D_LIB") or os.path.join(HERE, "lib", "libpose6d.so")
 HEADER = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "pose6d.h")
 
 DT_F32 = 0
