@@ -44,59 +44,6 @@ __device__ __forceinline__ void store_vec(T* p, const float* f) {
 }
 
 // ---------------------------------------------------------------- finalize
-// Chan et al. parallel variance: merge (n, mean, M2) with (nb, mean_b, M2_b)
-struct Welford {
-  double n, mean, m2;
-};
-__device__ __forceinline__ void merge(Welford& a, double nb, double mb, double qb) {
-  if (nb <= 0.0) return;
-  const double n = a.n + nb, d = mb - a.mean;
-  a.mean += d * nb / n;
-  a.m2 += qb + d * d * a.n * nb / n;
-  a.n = n;
-}
-
-constexpr int kSplits = 64;   // stage-1 row chunks
-
-// stage 1: grid (ceil(C/16), splits); rows are the conv epilogue's 32-pixel partials
-// (sum, M2); block = 16 channels x 16 lanes merges its chunk of rows (lane l takes
-// rows l, l+16, ... two loads in flight), lane 0 merges the lanes in order
-// -> ws[split][3][C] = (n, mean, M2)
-__global__ __launch_bounds__(kThreads) void bn_stats_stage1_kernel(const float* __restrict__ part, int rows, int C,
-                                                                   int64_t M, double* __restrict__ ws) {
-  __shared__ double red[3][16][17];
-  const int cl = threadIdx.x & 15, ln = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
-  const int s = blockIdx.y, S = gridDim.y;
-  const int r0 = (int)((int64_t)rows * s / S), r1 = (int)((int64_t)rows * (s + 1) / S);
-  Welford w{0.0, 0.0, 0.0};
-  if (c < C) {
-    int r = r0 + ln;
-    for (; r + 16 < r1; r += 32) {
-      const float s0 = part[(int64_t)c * rows + r], q0 = part[((int64_t)C + c) * rows + r];
-      const float s1 = part[(int64_t)c * rows + r + 16], q1 = part[((int64_t)C + c) * rows + r + 16];
-      const double n0 = (double)min((int64_t)32, M - (int64_t)r * 32);
-      const double n1 = (double)min((int64_t)32, M - (int64_t)(r + 16) * 32);
-      merge(w, n0, (double)s0 / n0, (double)q0);
-      merge(w, n1, (double)s1 / n1, (double)q1);
-    }
-    if (r < r1) {
-      const double nb = (double)min((int64_t)32, M - (int64_t)r * 32);
-      merge(w, nb, (double)part[(int64_t)c * rows + r] / nb, (double)part[((int64_t)C + c) * rows + r]);
-    }
-  }
-  red[0][cl][ln] = w.n;
-  red[1][cl][ln] = w.mean;
-  red[2][cl][ln] = w.m2;
-  __syncthreads();
-  if (ln == 0 && c < C) {
-    for (int k = 1; k < 16; ++k) merge(w, red[0][cl][k], red[1][cl][k], red[2][cl][k]);
-    ws[((int64_t)s * 3 + 0) * C + c] = w.n;
-    ws[((int64_t)s * 3 + 1) * C + c] = w.mean;
-    ws[((int64_t)s * 3 + 2) * C + c] = w.m2;
-  }
-}
-
 // ONE launch (training): block = 256 / L channels x L lanes (L = 64 or 256 by the
 // row count); lane l folds partial rows l, l + L, ... of its channel as shifted
 // sums about K = row 0's mean:
@@ -186,62 +133,27 @@ __global__ __launch_bounds__(kThreads) void bn_stats_finalize_kernel(
   }
 }
 
-// stage 2 (training): merge the splits in order -> batch mean / biased var
-__global__ __launch_bounds__(kThreads) void bn_finalize_kernel(
-    const double* __restrict__ ws, int splits, int C, double count, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
-    float momentum, float eps, int training, float* __restrict__ scale, float* __restrict__ shift,
-    float* __restrict__ smean, float* __restrict__ sinv) {
-  // block = 16 channels x 16 lanes; lane l merges splits l, l+16, ... (loads issued
-  // together), then lane 0 merges the 16 lane results in order (deterministic)
-  __shared__ double red[3][16][17];
-  const int cl = threadIdx.x & 15, ln = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
-  if (training) {
-    Welford w{0.0, 0.0, 0.0};
-    if (c < C) {
-      double v[kSplits / 16][3];
-#pragma unroll
-      for (int i = 0; i < kSplits / 16; ++i) {
-        const int s = ln + 16 * i;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) v[i][k] = s < splits ? ws[((int64_t)s * 3 + k) * C + c] : 0.0;
-      }
-#pragma unroll
-      for (int i = 0; i < kSplits / 16; ++i) merge(w, v[i][0], v[i][1], v[i][2]);
-    }
-    red[0][cl][ln] = w.n;
-    red[1][cl][ln] = w.mean;
-    red[2][cl][ln] = w.m2;
-    __syncthreads();
-    if (ln == 0 && c < C) {
-      for (int k = 1; k < 16; ++k) merge(w, red[0][cl][k], red[1][cl][k], red[2][cl][k]);
-      const double mean = w.mean;
-      double var = w.m2 / count;
-      if (var < 0.0) var = 0.0;
-      const float inv = (float)(1.0 / sqrt(var + (double)eps));
-      const float sc = gamma[c] * inv;
-      scale[c] = sc;
-      shift[c] = beta[c] - (float)mean * sc;
-      smean[c] = (float)mean;
-      sinv[c] = inv;
-      const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
-      rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
-      rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) nbt[0] += 1;
-  } else if (c < C && ln == 0) {
-    const float inv = 1.0f / sqrtf(rvar[c] + eps);
-    const float sc = gamma[c] * inv;
-    scale[c] = sc;
-    shift[c] = beta[c] - rmean[c] * sc;
-    smean[c] = rmean[c];
-    sinv[c] = inv;
-  }
+// eval: running statistics -> scale / shift / saved mean / invstd (no partials)
+__global__ __launch_bounds__(kThreads) void bn_eval_finalize_kernel(const float* __restrict__ gamma,
+                                                                    const float* __restrict__ beta,
+                                                                    const float* __restrict__ rmean,
+                                                                    const float* __restrict__ rvar, int C, float eps,
+                                                                    float* __restrict__ scale,
+                                                                    float* __restrict__ shift,
+                                                                    float* __restrict__ smean,
+                                                                    float* __restrict__ sinv) {
+  const int c = blockIdx.x * kThreads + threadIdx.x;
+  if (c >= C) return;
+  const float inv = 1.0f / sqrtf(rvar[c] + eps);
+  const float sc = gamma[c] * inv;
+  scale[c] = sc;
+  shift[c] = beta[c] - rmean[c] * sc;
+  smean[c] = rmean[c];
+  sinv[c] = inv;
 }
 
 // ---------------------------------------------------------------- eval fold (all BNs, one launch)
-// the eval branch of bn_finalize_kernel for a table of BatchNorms (pose6d_bn_eval_fold)
+// bn_eval_finalize_kernel for a table of BatchNorms (pose6d_bn_eval_fold)
 struct EvalFold {
   const float *gamma, *beta, *rmean, *rvar;
   float *scale, *shift, *smean, *sinv;
@@ -538,10 +450,10 @@ extern "C" int pose6d_bn_finalize(const float* partial, int32_t rows, int32_t C,
                                   const float* beta, float* running_mean, float* running_var, int64_t* num_batches,
                                   float momentum, float eps, int32_t training, float* scale, float* shift,
                                   float* save_mean, float* save_invstd, double* workspace, void* stream) {
-  P6_CHECK_ARG(C > 0 && (!training || (rows > 0 && count > 0 && workspace)), "pose6d_bn_finalize: bad sizes");
+  (void)workspace;   // kept in the ABI; the single-launch finalize needs none
+  P6_CHECK_ARG(C > 0 && (!training || (rows > 0 && count > 0)), "pose6d_bn_finalize: bad sizes");
   hipStream_t s = p6::stream_of(stream);
-  int splits = 0;
-  if (training && getenv("POSE6D_BN_TWO_STAGE") == nullptr) {
+  if (training) {
     if (rows > 512)
       bn_stats_finalize_kernel<256><<<C, kThreads, 0, s>>>(partial, rows, C, count, gamma, beta, running_mean,
                                                             running_var, num_batches, momentum, eps, scale, shift,
@@ -551,17 +463,10 @@ extern "C" int pose6d_bn_finalize(const float* partial, int32_t rows, int32_t C,
                                                                           running_mean, running_var, num_batches,
                                                                           momentum, eps, scale, shift, save_mean,
                                                                           save_invstd);
-    P6_LAUNCH_CHECK();
-    return POSE6D_OK;
+  } else {
+    bn_eval_finalize_kernel<<<p6::ceil_div(C, kThreads), kThreads, 0, s>>>(gamma, beta, running_mean, running_var, C,
+                                                                          eps, scale, shift, save_mean, save_invstd);
   }
-  if (training) {
-    splits = rows < kSplits ? rows : kSplits;
-    bn_stats_stage1_kernel<<<dim3(p6::ceil_div(C, 16), splits), kThreads, 0, s>>>(partial, rows, C, count, workspace);
-    P6_LAUNCH_CHECK();
-  }
-  bn_finalize_kernel<<<p6::ceil_div(C, 16), kThreads, 0, s>>>(
-      workspace, splits, C, (double)count, gamma, beta, running_mean, running_var, num_batches, momentum, eps, training,
-      scale, shift, save_mean, save_invstd);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }

@@ -249,7 +249,7 @@ class TrunkEngine:
             if isinstance(op, _ActOp):
                 op.bn_ready = None
         self.ws_bn = f32(max(ws_bn, 1))
-        self.ws_fin = torch.empty(64 * 3 * max(op.cout for op in self.convs), device=device, dtype=torch.float64)
+        self.ws_fin = None   # pose6d_bn_finalize needs no workspace (one launch)
         self.feat = f32(B, self.feat_dim)
         self.feat_grad_in = None
         self._fold_dev, self._fold_key = None, None

@@ -270,8 +270,7 @@ int pose6d_bwd_variant(int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t C
  * stats, num_batches_tracked updated in training (torch semantics).
  * partial: [2][C][rows] (rows = ceil(count / 32); sum, M2 about the block's mean)
  * over 32-pixel blocks, as pose6d_conv2d_fwd writes them, folded in fp64 as shifted sums about the first row's
- * mean in ONE launch (env POSE6D_BN_TWO_STAGE: the earlier two-launch Chan
- * merge); workspace: 64 * 3 * C doubles (used by the two-stage form only). */
+ * mean in ONE launch; workspace: unused (kept in the ABI, may be NULL). */
 int pose6d_bn_finalize(const float *partial, int32_t rows, int32_t C, int64_t count, const float *gamma,
                        const float *beta, float *running_mean, float *running_var, int64_t *num_batches,
                        float momentum, float eps, int32_t training, float *scale, float *shift, float *save_mean,
