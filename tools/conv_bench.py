@@ -94,6 +94,8 @@ def main():
                          device=dev)
         dw = torch.empty(Cout, Cin, k, k, device=dev)
         flops = 2.0 * B * Ho * Wo * Cout * Cin * k * k
+        sc, sh = torch.rand(Cout, device=dev) + 0.5, torch.randn(Cout, device=dev) * 0.1
+        res = torch.randn(B, Ho, Wo, Cout, device=dev).to(dtype) if "fwdactres" in a.passes else None
         fns = {
             "fwd": lambda: call("conv2d_fwd", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream()),
             # no BN statistics (as in eval without the fold)
@@ -103,6 +105,11 @@ def main():
             "fwdcold": lambda: (flush.zero_(), call("conv2d_fwd", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k,
                                                     k, s, p, Ho, Wo, stream())),
             "flush": lambda: flush.zero_(),
+            # eval epilogue: BN (+ residual) + ReLU applied before the store (pose6d_conv2d_fwd_act)
+            "fwdact": lambda: call("conv2d_fwd_act", dt, x, wp, None, y, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, sc,
+                                   sh, None, None, None, 1, stream()),
+            "fwdactres": lambda: call("conv2d_fwd_act", dt, x, wp, None, y, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo,
+                                      sc, sh, res, None, None, 1, stream()),
             "dgrad": lambda: call("conv2d_dgrad", dt, dy, wt, None, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream()),
             "dgradip": lambda: call("conv2d_dgrad", dt, dy, wt, dx, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream()),
             "bwdip": lambda: call("conv2d_backward", dt, x, dy, wt, dx, dx, dw, 0, ws, ws.numel() * 4, B, H, W, Cin,
