@@ -421,7 +421,9 @@ __global__ __launch_bounds__(kThreads) void channel_sum_kernel(const T* __restri
 
 inline unsigned grid_for(int64_t chunks) {
   int64_t b = (chunks + kThreads - 1) / kThreads;
-  if (b > 4096) b = 4096;
+  // one chunk per thread for every ResNet50 activation at batch 32 (<= 12544 blocks): a
+  // grid-stride trip after the first would wait for the previous trip's stores
+  if (b > 65535) b = 65535;
   if (b < 1) b = 1;
   return (unsigned)b;
 }

@@ -77,17 +77,47 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float* __restrict__ p, 
   const float step_size = lr / bc1;
   const float bc2s = sqrtf(bc2);
   const float decay = 1.f - lr * wd;
-  for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
-    const float gi = g[i] * coef;
-    float pi = p[i] * decay;
-    float mi = m[i];
+  auto upd = [&](float& pi, float& mi, float& vi, float graw) {
+    const float gi = graw * coef;
+    pi = pi * decay;
     mi = mi + (1.f - b1) * (gi - mi);                 // exp_avg.lerp_(grad, 1 - beta1)
-    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;  // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
+    vi = vi * b2 + (1.f - b2) * gi * gi;              // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
     const float denom = sqrtf(vi) / bc2s + eps;
     pi = pi - step_size * (mi / denom);
-    p[i] = pi;
-    m[i] = mi;
-    v[i] = vi;
+  };
+  // float4 chunks, U per trip with every load of the trip issued before the first
+  // store: a load issued after a store is waited for with vmcnt(0), i.e. behind that
+  // store's acknowledgement (one memory round trip per trip instead of per element)
+  constexpr int U = 4;
+  const int64_t n4 = n / 4, stride = (int64_t)gridDim.x * kThreads;
+  float4* p4 = reinterpret_cast<float4*>(p);
+  float4* m4 = reinterpret_cast<float4*>(m);
+  float4* v4 = reinterpret_cast<float4*>(v);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (int64_t i0 = blockIdx.x * (int64_t)kThreads + threadIdx.x; i0 < n4; i0 += U * stride) {
+    float4 pv[U], mv[U], vv[U], gv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride < n4 ? i0 + u * stride : i0;
+      gv[u] = g4[i]; pv[u] = p4[i]; mv[u] = m4[i]; vv[u] = v4[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      upd(pv[u].x, mv[u].x, vv[u].x, gv[u].x);
+      upd(pv[u].y, mv[u].y, vv[u].y, gv[u].y);
+      upd(pv[u].z, mv[u].z, vv[u].z, gv[u].z);
+      upd(pv[u].w, mv[u].w, vv[u].w, gv[u].w);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i < n4) { p4[i] = pv[u]; m4[i] = mv[u]; v4[i] = vv[u]; }
+    }
+  }
+  for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)kThreads + threadIdx.x; i < n; i += stride) {
+    float pi = p[i], mi = m[i], vi = v[i];
+    upd(pi, mi, vi, g[i]);
+    p[i] = pi; m[i] = mi; v[i] = vi;
   }
 }
 
@@ -112,8 +142,12 @@ extern "C" int pose6d_adamw_step(float* param, const float* grad, float* exp_avg
                                  const float* partials, int32_t nparts, const float* hp, float* norm_out,
                                  void* stream) {
   if (n == 0) return POSE6D_OK;
-  int64_t blocks = (n + kThreads * 4 - 1) / (kThreads * 4);
-  if (blocks > 4096) blocks = 4096;
+  P6_CHECK_ARG(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0,
+               "pose6d_adamw_step: buffers must be 16-byte aligned");
+  // one trip of U = 4 float4 per thread for up to 64 M parameters (each block re-reads
+  // the clip partials: a few KiB, L2-resident)
+  int64_t blocks = (n + kThreads * 16 - 1) / (kThreads * 16);
+  if (blocks > 16384) blocks = 16384;
   adamw_kernel<<<(unsigned)blocks, kThreads, 0, p6::stream_of(stream)>>>(param, grad, exp_avg, exp_avg_sq, n, partials,
                                                                         nparts, hp, norm_out);
   P6_LAUNCH_CHECK();
