@@ -35,7 +35,11 @@ template <> struct KT<float> { static constexpr int VEC = 4; static constexpr in
 // kDgradS2: stride-2 data gradient split into the four output parity classes
 // (y & 1, x & 1); each class only gathers the taps that reach it, so no MAC is
 // spent on the zeros a masked stride-2 gather would multiply.
-enum Mode { kGemm = 0, kFwd = 1, kFwdNarrow = 2, kDgrad = 3, kDgradS2 = 4 };
+// kGemmDual (eval only): a bottleneck's last 1x1 conv and its downsample branch in one
+// launch -- K-steps [0, Kpad) are the block's 1x1 GEMM over src, the rest the 1x1
+// (stride2) downsample over src2 with weights wts2, summed into a second accumulator
+// set; the epilogue applies both BatchNorms exactly as the separate launches did.
+enum Mode { kGemm = 0, kFwd = 1, kFwdNarrow = 2, kDgrad = 3, kDgradS2 = 4, kGemmDual = 5 };
 
 struct Geom {
   int M, Ncols, K, Kpad;   // GEMM dims; Kpad = weight row length
@@ -54,6 +58,11 @@ struct Geom {
   // byte per 16-byte chunk: pose6d_bn_act_fwd_mask's ReLU bits), i.e. the masked dout
   // of the block's last BN, instead of a materialised dz (null = res as is)
   const uint8_t* res_mask;
+  // kGemmDual: the downsample operand [N][SH2][SW2][Kpad2], its packed weights
+  // [Ncols][Kpad2], its stride (rows m = (n, oy, ox) of the RH x RW output grid)
+  const void* src2;
+  const void* wts2;
+  int Kpad2, SH2, SW2, stride2;
 };
 
 // kDgradS2 launched in place (dres == dx) when a single parity class has taps
@@ -120,11 +129,12 @@ __device__ __forceinline__ void load_f32s(const float* __restrict__ p, float (&f
 
 template <int NW> struct WaveGrid { static constexpr int WM = NW / 2, WN = 2, NT = 64 * NW; };
 
-template <typename T, int BM, int BN, bool BNF = false, int ACT = 0, int NW = 4>
+template <typename T, int BM, int BN, bool BNF = false, int ACT = 0, int NW = 4, bool DUAL = false>
 __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / (16 * (NW / 2))][BN / 32], char* smem, const Geom& g,
                                               const float* __restrict__ bias, const T* __restrict__ res,
                                               T* __restrict__ out, float* __restrict__ stats, int m0, int n0,
-                                              int cls = -1, const BnBwd* bn = nullptr, int prow = 0) {
+                                              int cls = -1, const BnBwd* bn = nullptr, int prow = 0,
+                                              const f32x4 (*acc2)[BN / 32] = nullptr) {
   constexpr int WM = WaveGrid<NW>::WM, NT = WaveGrid<NW>::NT;
   constexpr int TM = BM / (16 * WM), TN = BN / 32;
   static_assert(TM % 2 == 0, "BatchNorm partials cover 32-row blocks of one wave");
@@ -246,6 +256,9 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / (16 * (NW / 2))]
         const int lr = wm * (BM / WM) + i * 16 + fc * 4 + r;
         const int lc = wn * (BN / 2) + j * 16 + fr;
         *reinterpret_cast<T*>(smem + lr * CROW + lc * (int)sizeof(T)) = p6::from_f<T>(acc[i][j][r]);
+        // kGemmDual: the downsample branch's tile, rounded to T as its own launch stored it
+        if constexpr (DUAL)
+          *reinterpret_cast<T*>(smem + (BM + lr) * CROW + lc * (int)sizeof(T)) = p6::from_f<T>(acc2[i][j][r]);
       }
   float asc[E], ash[E], arsc[E], arsh[E];
   // (issued after the accumulators are staged: their registers are free again)
@@ -283,11 +296,16 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / (16 * (NW / 2))]
       // pose6d_bn_act_fwd's arithmetic on the stored (T-rounded) conv output
       T a[E], b[E];
       __builtin_memcpy(a, &v, 16);
-      __builtin_memcpy(b, &rv[it], 16);
+      if constexpr (DUAL) {
+        const uint4 dv = *reinterpret_cast<const uint4*>(smem + (BM + lr) * CROW + cc * 16);
+        __builtin_memcpy(b, &dv, 16);
+      } else {
+        __builtin_memcpy(b, &rv[it], 16);
+      }
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         float x = fmaf(p6::to_f(a[e]), asc[e], ash[e]);
-        if (res) x += g.act_rscale ? fmaf(p6::to_f(b[e]), arsc[e], arsh[e]) : p6::to_f(b[e]);
+        if (DUAL || res) x += g.act_rscale ? fmaf(p6::to_f(b[e]), arsc[e], arsh[e]) : p6::to_f(b[e]);
         if (g.act_relu) x = fmaxf(x, 0.f);
         a[e] = p6::from_f<T>(x);
       }
@@ -667,7 +685,10 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   // parity class (kDgradS2): the four classes of one tile are consecutive logical
   // ids, so every XCD gets an even share of the heavy and the empty classes and the
   // four blocks that gather the same dY rows run on the same L2
+  constexpr bool DUAL = MODE == kGemmDual;
   int cls = -1, py = 0, px = 0, kh0 = 0, kw0 = 0, ntx = 1, nk = g.Kpad >> LOG_KS;
+  const int nk1 = nk;   // kGemmDual: K-steps of the first (block) GEMM
+  if (DUAL) nk += g.Kpad2 >> LOG_KS;
   if (MODE == kDgradS2) {
     if (g.s2one) {
       cls = g.s2one - 1;
@@ -697,6 +718,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
 
   // rows this lane DMAs: row = i*RW + wave*8 + r8; it fetches logical chunk pch ^ swz8(row)
   int a_pix[A_INS], a_y[A_INS], a_x[A_INS], a_ck[A_INS];
+  int a_pix2[DUAL ? A_INS : 1];   // kGemmDual: the row's pixel in the downsample operand
   bool a_ok[A_INS];
 #pragma unroll
   for (int i = 0; i < A_INS; ++i) {
@@ -705,8 +727,14 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
     a_ok[i] = m < g.M;
     a_ck[i] = (pch ^ swz8(row)) * CH;
     const int mm = a_ok[i] ? m : 0;
-    if (MODE == kGemm) {
+    if (MODE == kGemm || DUAL) {
       a_pix[i] = mm; a_y[i] = 0; a_x[i] = 0;
+      if constexpr (DUAL) {
+        const int hw = g.RH * g.RW;
+        const int n = mm / hw, rem = mm - n * hw;
+        const int y = rem / g.RW, x = rem - y * g.RW;
+        a_pix2[i] = (n * g.SH2 + y * g.stride2) * g.SW2 + x * g.stride2;
+      }
     } else {
       const int hw = g.RH * g.RW;
       const int n = mm / hw, rem = mm - n * hw;
@@ -728,6 +756,18 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
     b_base[j] = ok ? wts + (int64_t)n * g.Kpad + (pch ^ swz8(row)) * CH : reinterpret_cast<const T*>(zp);
     b_mask[j] = ok ? ~0u : 0u;
   }
+  // kGemmDual: the downsample weights' rows, switched to after the first GEMM's K-steps
+  const T* b_base2[DUAL ? B_INS : 1];
+  if constexpr (DUAL) {
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j) {
+      const int row = j * RW + wave * 8 + r8;
+      const int n = n0 + row;
+      b_base2[j] = n < g.Ncols ? reinterpret_cast<const T*>(g.wts2) + (int64_t)n * g.Kpad2 + (pch ^ swz8(row)) * CH
+                               : reinterpret_cast<const T*>(zp);
+    }
+  }
+  int phase = 0;   // kGemmDual: 0 = block GEMM, 1 = downsample GEMM
 
   // The K loop walks filter taps in order; inside a tap the 64-deep slices are
   // contiguous channels.  Row source pointers (and their validity: padding, rows
@@ -735,7 +775,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   // there (uniform branch) and each K-step only adds the channel offset c0 --
   // the per-step address arithmetic that made these kernels issue-bound at one
   // workgroup per CU.  issue() is called with consecutive kt.
-  const int tap_len = MODE == kGemm ? g.Kpad : g.SC;
+  int tap_len = (MODE == kGemm || DUAL) ? g.Kpad : g.SC;
   int c0 = 0, kh = kh0, kw = kw0, tw = 0, tap_koff = MODE == kDgradS2 ? (kh0 * g.KW + kw0) * g.SC : 0;
   const T* a_base[A_INS];
   unsigned a_mask[A_INS];
@@ -744,8 +784,16 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
     for (int i = 0; i < A_INS; ++i) {
       bool ok = a_ok[i];
       int64_t off = 0;
-      if (MODE == kGemm) {
+      if (MODE == kGemm || DUAL) {
         off = (int64_t)a_pix[i] * g.K;
+        if constexpr (DUAL) {
+          if (phase) {
+            off = (int64_t)a_pix2[i] * g.Kpad2;
+            a_base[i] = ok ? reinterpret_cast<const T*>(g.src2) + off + a_ck[i] : reinterpret_cast<const T*>(zp);
+            a_mask[i] = ok ? ~0u : 0u;
+            continue;
+          }
+        }
       } else {
         int sy, sx;
         if (MODE == kFwd) {
@@ -775,12 +823,21 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
     if (c0 == 0) set_tap();
     const unsigned boff = (unsigned)(tap_koff + c0);
 #pragma unroll
-    for (int j = 0; j < B_INS; ++j) glds16(b_base[j] + (boff & b_mask[j]), Bs + (j * RW + wave * 8) * 128);
+    for (int j = 0; j < B_INS; ++j) {
+      const T* bb = b_base[j];
+      if constexpr (DUAL) bb = phase ? b_base2[j] : b_base[j];
+      glds16(bb + (boff & b_mask[j]), Bs + (j * RW + wave * 8) * 128);
+    }
 #pragma unroll
     for (int i = 0; i < A_INS; ++i) glds16(a_base[i] + ((unsigned)c0 & a_mask[i]), As + (i * RW + wave * 8) * 128);
     c0 += KS;
     if (c0 == tap_len) {
       c0 = 0;
+      if constexpr (DUAL) {
+        phase = 1;
+        tap_len = g.Kpad2;
+        return;
+      }
       if (MODE == kDgradS2) {
         kw += 2;
         if (++tw == ntx) { tw = 0; kw = kw0; kh += 2; }
@@ -793,6 +850,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   };
 
   f32x4 acc[TM][TN];
+  f32x4 acc2[DUAL ? TM : 1][DUAL ? TN : 1];   // kGemmDual: the block GEMM's sums, parked
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -817,7 +875,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   const unsigned ring_base = lds_addr(smem);
   // mid(): issued between the fragment reads and their wait, so the next stage's
   // LDS-DMA issue (tens of cycles per instruction) overlaps the LDS read latency
-  auto compute = [&](int buf, auto&& mid) {
+  auto compute = [&](int buf, auto&& mid, auto& acc) {
     const unsigned slot = ring_base + buf * STAGE;
     if constexpr (TM + TN == 4 && kPairedFrags) {
       unsigned addr[2][4];
@@ -860,15 +918,33 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   for (int kt = 0; kt < nk; ++kt) {
     const int left = nk - 1 - kt;
     wait_ahead<LOADS, S - 2>(left < S - 2 ? left : S - 2);   // stage kt landed, for every wave
-    compute(cur, [&]() {
+    auto mid = [&]() {
       if (kt + S - 1 < nk) issue(kt + S - 1, wbuf);
-    });
+    };
+    if constexpr (DUAL) {
+      // the block GEMM is complete: park its sums, accumulate the downsample afresh
+      // (one accumulator set in the loop keeps the register budget of the plain kernel)
+      if (kt == nk1) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc2[i][j] = acc[i][j];
+            acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+      }
+    }
+    compute(cur, mid, acc);
     cur = cur == S - 1 ? 0 : cur + 1;
     wbuf = wbuf == S - 1 ? 0 : wbuf + 1;
   }
   asm volatile("s_barrier" ::: "memory");   // every wave done reading the ring before the epilogue reuses it
-  conv_epilogue<T, BM, BN, BNF, ACT ? 1 : 0, NW>(acc, smem, g, bias, res, out, stats, m0, n0, cls, bn,
-                                   MODE == kDgradS2 ? tm * 4 + cls : tm);
+  if constexpr (DUAL)   // acc2 = the block GEMM, acc = the downsample branch
+    conv_epilogue<T, BM, BN, false, 1, NW, true>(acc2, smem, g, bias, nullptr, out, nullptr, m0, n0, -1, nullptr, 0,
+                                                 acc);
+  else
+    conv_epilogue<T, BM, BN, BNF, ACT ? 1 : 0, NW>(acc, smem, g, bias, res, out, stats, m0, n0, cls, bn,
+                                                   MODE == kDgradS2 ? tm * 4 + cls : tm);
 }
 
 template <typename T, int BM, int BN, int MODE, int S, bool ACT, int NW>
@@ -909,6 +985,7 @@ __global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const bf16* __restri
 // K-steps of the longest work item (kDgradS2: the class with the most taps);
 // ks = elements per K-step (64 bf16, 32 fp32)
 int fast_nk(int mode, const Geom& g, int ks = 64) {
+  if (mode == kGemmDual) return (g.Kpad + g.Kpad2) / ks;
   if (mode != kDgradS2) return g.Kpad / ks;
   int best = 0;
   for (int cls = 0; cls < 4; ++cls) {
@@ -932,11 +1009,12 @@ int launch_fast(const Geom& g0, const void* src, const void* w, const float* bia
   g.gn = p6::ceil_div(g.Ncols, BN);
   const int nk = fast_nk(MODE, g, LK<T>::KS);
   const int ring = (nk < S ? (nk > 0 ? nk : 1) : S) * (BM + BN) * 128;
-  const int epi = BM * (BN * (int)sizeof(T) + 16);
+  // kGemmDual stages both branches' tiles for its epilogue
+  const int epi = (MODE == kGemmDual ? 2 : 1) * BM * (BN * (int)sizeof(T) + 16);
   const int lds = ring > epi ? ring : epi;
   if (MODE == kDgradS2) s2_single_class(g, res, out);
   const int grid = g.gm * g.gn * (MODE == kDgradS2 ? s2_classes(g) : 1);
-  if constexpr (MODE == kGemm || MODE == kFwd) {
+  if constexpr (MODE == kGemm || MODE == kFwd || MODE == kGemmDual) {
     if (g.act) {   // eval BN-act epilogue (pose6d_conv2d_fwd_act)
       conv_lds_kernel<T, BM, BN, MODE, S, true, NW><<<grid, 64 * NW, lds, s>>>((const T*)src, (const T*)w, bias,
                                                                                (const T*)res, (T*)out, stats, g);
@@ -983,6 +1061,7 @@ int dispatch_fast_t(int mode, const Geom& g, int tile, int stages, const void* s
     case kGemm: return launch_fast_mode<T, kGemm>(g, tile, stages, src, w, bias, res, out, stats, s);
     case kFwd: return launch_fast_mode<T, kFwd>(g, tile, stages, src, w, bias, res, out, stats, s);
     case kDgradS2: return launch_fast_mode<T, kDgradS2>(g, tile, stages, src, w, bias, res, out, stats, s);
+    case kGemmDual: return launch_fast_s<T, 64, 64, kGemmDual>(g, stages, src, w, bias, res, out, stats, s);
     default: return launch_fast_mode<T, kDgrad>(g, tile, stages, src, w, bias, res, out, stats, s);
   }
 }
@@ -1071,6 +1150,10 @@ int env_int(const char* name, int dflt);
 // (tuning / A-B experiments only).
 bool fast_ok(int dtype, int mode, const Geom& g) {
   if (mode == kFwdNarrow) return false;
+  if (mode == kGemmDual) {
+    const int ks2 = dtype == POSE6D_DT_BF16 ? 64 : 32;
+    return g.K % ks2 == 0 && g.Kpad == g.K && g.Kpad2 % ks2 == 0;
+  }
   if (dtype == POSE6D_DT_F32 && env_int("POSE6D_CONV_F32_FAST", 1) == 0) return false;
   const int ks = dtype == POSE6D_DT_BF16 ? 64 : 32;   // elements per 128-byte K-step
   if (g.K % ks != 0 || g.Kpad != g.K) return false;
@@ -1132,7 +1215,7 @@ Plan choose(int dtype, int mode, const Geom& g, bool fused = false) {
     const char* ord = getenv("POSE6D_CONV_ORDER");
     p.g.nmajor = ord && ord[0] == 'n';
   }
-  p.tile = fused ? 3 : env_int("POSE6D_CONV_TILE", pick_tile_fast(dtype, p.g.M, g.Ncols, g.K));
+  p.tile = (fused || mode == kGemmDual) ? 3 : env_int("POSE6D_CONV_TILE", pick_tile_fast(dtype, p.g.M, g.Ncols, g.K));
   if (p.tile == 2) p.tile = 3;   // no 64x128 instance on the fast path
   // two slots (32 KiB at 64x64) keep several workgroups per CU resident, which hides
   // the DMA latency better than a deeper ring; only long-K grids that leave CUs
@@ -1232,6 +1315,39 @@ extern "C" int pose6d_conv2d_fwd_act(int32_t dtype, const void* x, const void* w
   g.act_rscale = res_scale;
   g.act_rshift = res_shift;
   return run_conv(dtype, mode, g, x, w, bias, res, out, nullptr, p6::stream_of(stream));
+}
+
+extern "C" int pose6d_conv2d_fwd_act_dual(int32_t dtype, const void* x, const void* w, const void* xd, const void* wd,
+                                          void* out, int32_t N, int32_t Ho, int32_t Wo, int32_t Cin, int32_t Cout,
+                                          int32_t Hd, int32_t Wd, int32_t Cind, int32_t stride_d, const float* scale,
+                                          const float* shift, const float* scale_d, const float* shift_d,
+                                          int32_t relu, void* stream) {
+  P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_fwd_act_dual: bad dtype %d", dtype);
+  P6_CHECK_ARG(N > 0 && Ho > 0 && Wo > 0 && Cout > 0 && Cout % 8 == 0, "pose6d_conv2d_fwd_act_dual: bad shape");
+  P6_CHECK_ARG(stride_d >= 1 && Ho == (Hd - 1) / stride_d + 1 && Wo == (Wd - 1) / stride_d + 1,
+               "pose6d_conv2d_fwd_act_dual: downsample geometry inconsistent");
+  P6_CHECK_ARG(scale && shift && scale_d && shift_d, "pose6d_conv2d_fwd_act_dual: null BatchNorm scale / shift");
+  const int ks = dtype == POSE6D_DT_BF16 ? 64 : 32;
+  P6_CHECK_ARG(Cin % ks == 0 && Cind % ks == 0, "pose6d_conv2d_fwd_act_dual: Cin and Cind must be multiples of %d",
+               ks);
+  int mode;
+  Geom g = fwd_geom(dtype, N, Ho, Wo, Cin, Cout, 1, 1, 1, 0, Ho, Wo, &mode);
+  g.src2 = xd;
+  g.wts2 = wd;
+  g.Kpad2 = Cind;
+  g.SH2 = Hd;
+  g.SW2 = Wd;
+  g.stride2 = stride_d;
+  g.act = 1;
+  g.act_relu = relu != 0;
+  g.act_scale = scale;
+  g.act_shift = shift;
+  g.act_rscale = scale_d;
+  g.act_rshift = shift_d;
+  const Plan p = choose(dtype, kGemmDual, g);
+  P6_CHECK_ARG(p.fast, "pose6d_conv2d_fwd_act_dual: shape outside the LDS-DMA path");
+  return dispatch_fast(dtype, kGemmDual, p.g, p.tile, p.stages, x, w, nullptr, nullptr, out, nullptr,
+                       p6::stream_of(stream));
 }
 
 namespace {

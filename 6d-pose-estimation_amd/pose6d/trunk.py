@@ -321,10 +321,21 @@ class TrunkEngine:
         # eval: the BN (running statistics) is known before the conv runs, so the conv's
         # epilogue applies BN (+ residual) + ReLU and stores the activation directly
         fold = not training and os.environ.get("POSE6D_EVAL_FUSE", "1") != "0"
+        dual = {}
         if fold:
             self._eval_fold(st)
+            dual = self._dual_pairs()
         for op in self.ops:
             if isinstance(op, _ConvOp):
+                if op in dual:
+                    if dual[op] is None:
+                        continue   # a downsample conv: computed inside its block's last conv launch
+                    a = op.act_op
+                    r = a.res_conv
+                    call("conv2d_fwd_act_dual", dt, op.src.t, op.wp, r.src.t, r.wp, a.out.t, B, op.Ho, op.Wo,
+                         op.cin_pad, op.cout, r.H, r.W, r.cin_pad, r.stride, op.scale, op.shift, r.scale, r.shift,
+                         int(a.relu), st)
+                    continue
                 bias = op.conv.bias
                 bias = bias.detach() if bias is not None else None
                 bn = op.bn
@@ -373,6 +384,34 @@ class TrunkEngine:
         self.generation += 1
         self._saved_gen = self.generation if training else -1
         return self.feat
+
+    def _dual_pairs(self):
+        """Eval: each Bottleneck with a downsample branch gets its output from ONE launch
+        (pose6d_conv2d_fwd_act_dual: conv3 and the downsample conv as two GEMMs of one
+        workgroup, both BatchNorms + add + ReLU in the epilogue; bit-identical to the
+        separate launches) -- the downsample output never makes an HBM round trip.
+        Only for the big-grid stages (layer1/layer2 at batch 32: >= 16384 output rows):
+        the pair runs on the 64x64 tile with both accumulator sets, which lost to the
+        separate launches (128x128 tiles) on layer3/layer4 (eval trace).
+        Returns {conv3: its downsample conv, downsample conv: None}; POSE6D_EVAL_DUAL=0
+        disables it, POSE6D_EVAL_DUAL_ROWS sets the row threshold."""
+        if os.environ.get("POSE6D_EVAL_DUAL", "1") == "0":
+            return {}
+        ks = 64 if self.dtype == torch.bfloat16 else 32
+        min_rows = int(os.environ.get("POSE6D_EVAL_DUAL_ROWS", "16384"))
+        pairs = {}
+        for op in self.ops:
+            if not isinstance(op, _ActOp) or op.res_conv is None or op.pooled:
+                continue
+            c3, r = op.cop, op.res_conv
+            ok = (c3.k == 1 and c3.stride == 1 and c3.pad == 0 and r.k == 1 and r.pad == 0
+                  and c3.conv.bias is None and r.conv.bias is None
+                  and c3.cin_pad % ks == 0 and r.cin_pad % ks == 0 and c3.cout == r.cout
+                  and (r.Ho, r.Wo) == (c3.Ho, c3.Wo) and self.B * c3.Ho * c3.Wo >= min_rows)
+            if ok:
+                pairs[c3] = r
+                pairs[r] = None
+        return pairs
 
     # ------------------------------------------------------------ backward
     def backward(self, dfeat, grad_of, accumulate=False, on_conv_done=None):

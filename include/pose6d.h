@@ -183,6 +183,18 @@ int pose6d_conv2d_fwd_act(int32_t dtype, const void *x, const void *w, const flo
                           int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
                           int32_t pad, int32_t Ho, int32_t Wo, const float *scale, const float *shift, const void *res,
                           const float *res_scale, const float *res_shift, int32_t relu, void *stream);
+/* eval-mode output of a torchvision Bottleneck with a downsample branch, ONE launch
+ * (replaces, at pose_net_*.py's `self.backbone(x)`, the block's conv3 + bn3 and the
+ * downsample conv + bn + add + ReLU):
+ *   out = act(T(x . w) * scale + shift + T(xd_s . wd) * scale_d + shift_d),
+ * x [N][Ho][Wo][Cin] (conv3 input), w [Cout][Cin]; xd [N][Hd][Wd][Cind] (block input),
+ * wd [Cout][Cind], xd_s = xd sampled every stride_d pixels; both 1x1, no bias.  Bit for
+ * bit pose6d_conv2d_fwd of the downsample then pose6d_conv2d_fwd_act with
+ * res_scale/res_shift, without the downsample output's HBM round trip. */
+int pose6d_conv2d_fwd_act_dual(int32_t dtype, const void *x, const void *w, const void *xd, const void *wd, void *out,
+                               int32_t N, int32_t Ho, int32_t Wo, int32_t Cin, int32_t Cout, int32_t Hd, int32_t Wd,
+                               int32_t Cind, int32_t stride_d, const float *scale, const float *shift,
+                               const float *scale_d, const float *shift_d, int32_t relu, void *stream);
 /* data gradient: dx [N][H][W][Cin] = conv_transpose(dy [N][Ho][Wo][Cout], wt) (+ dres if non-NULL).
  * dres may be dx itself (accumulate in place); a stride-2 1x1 conv then writes only the
  * pixels its taps reach (the other three parity classes are left as they are). */

@@ -56,3 +56,36 @@ def test_eval_bn_folded_into_conv_is_bit_identical(name, dtype, monkeypatch):
         torch.cuda.synchronize()
         outs.append((rot.clone(), trans.clone()))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_eval_downsample_in_block_launch_is_bit_identical(dtype, monkeypatch):
+    """Eval trunk with each downsampling Bottleneck's conv3 + downsample conv + both
+    BatchNorms + add + ReLU in ONE launch (pose6d_conv2d_fwd_act_dual) equals the
+    separate downsample launch + fused conv3 epilogue bit for bit (all four stages:
+    stride 1 at layer1, stride 2 at layers 2-4), with non-trivial running statistics."""
+    from pose6d.resnet import resnet50_trunk
+    from pose6d.trunk import TrunkEngine
+    torch.manual_seed(0)
+    seq = resnet50_trunk(3)
+    g = torch.Generator().manual_seed(11)
+    for mod in seq.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            C = mod.num_features
+            mod.running_mean.copy_(torch.randn(C, generator=g) * 0.1)
+            mod.running_var.copy_(torch.rand(C, generator=g) + 0.5)
+            mod.weight.data.copy_(torch.rand(C, generator=g) + 0.5)
+            mod.bias.data.copy_(torch.randn(C, generator=g) * 0.1)
+    seq = seq.cuda().eval()
+    eng = TrunkEngine(seq, 3)
+    eng.set_dtype(dtype)
+    x = torch.randn(4, 3, 224, 224, generator=g).cuda()
+    monkeypatch.setenv("POSE6D_EVAL_DUAL_ROWS", "0")   # every stage (batch 4 grids are small)
+    feats = []
+    for dual in ("0", "1"):
+        monkeypatch.setenv("POSE6D_EVAL_DUAL", dual)
+        with torch.no_grad():
+            feats.append(eng.forward(x, False).clone())
+        torch.cuda.synchronize()
+    assert len(eng._dual_pairs()) == 8   # 4 blocks x (conv3, downsample)
+    assert torch.equal(feats[0], feats[1])
