@@ -83,19 +83,40 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_kernel(const float* __restr
 // rows of 64 B.  Inside a 16-deep K chunk lane (r, q) feeds MFMA step s with
 // k = 4 q + s, so A and (BKC) B fragments are single 16-byte loads; the
 // reduction order differs from torch's but all products are exact fp32.
+// eval BatchNorm1d (+ ReLU) applied to a Linear's output before it is stored
+// (pose6d_gemm_f32_bn_eval): bn1d_fwd_kernel's eval arithmetic, term for term
+struct BnEv {
+  const float *gamma, *beta, *rmean, *rvar;
+  float eps;
+  int relu, on;
+};
+__device__ __forceinline__ float bn_eval_apply(float x, const BnEv& bn, int c) {
+  const float mean = bn.rmean[c];
+  const float inv = 1.0f / sqrtf(bn.rvar[c] + bn.eps);
+  float v = (x - mean) * inv * bn.gamma[c] + bn.beta[c];
+  if (bn.relu) v = fmaxf(v, 0.f);
+  return v;
+}
+
 constexpr int kSkW = 16;                      // waves per workgroup
 constexpr int kSkThreads = kSkW * 64;
 
+// Split K across workgroups (grid.y = K slices of `kchunk`, `part` = [slices][M][N]
+// partial sums, summed in slice order by gemm_splitk_reduce_kernel) when N / 16 column
+// groups alone would leave most CUs idle: a 2048 x 1024 weight streamed by 64
+// workgroups took ~15 us, i.e. ~0.5 TB/s.
 template <bool BKC, bool VEC>
 __global__ __launch_bounds__(kSkThreads) void skinny_gemm_kernel(
     const float* __restrict__ A, int64_t sam, const float* __restrict__ B, int64_t sbk, int64_t sbn,
-    float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, int M, int N, int K, float alpha, float beta) {
+    float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, int M, int N, int K, float alpha, float beta,
+    int kchunk, float* __restrict__ part, BnEv bn) {
   __shared__ float red[kSkW][32][17];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, q = lane >> 4;
   const int n0 = blockIdx.x * 16, n = n0 + r;
-  const int kc = ((K + kSkW - 1) / kSkW + 15) & ~15;
-  const int kb = w * kc, ke = min(K, kb + kc);
+  const int ks0 = blockIdx.y * kchunk, ks1 = min(K, ks0 + kchunk);
+  const int kc = ((ks1 - ks0 + kSkW - 1) / kSkW + 15) & ~15;
+  const int kb = ks0 + w * kc, ke = min(ks1, kb + kc);
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   const bool m0ok = r < M, m1ok = r + 16 < M, nok = n < N;
   for (int k = kb; k < ke; k += 16) {
@@ -144,9 +165,14 @@ __global__ __launch_bounds__(kSkThreads) void skinny_gemm_kernel(
       float t = 0.f;
 #pragma unroll
       for (int i = 0; i < kSkW; ++i) t += red[i][mm][cc];
+      if (part) {
+        part[((int64_t)blockIdx.y * M + mm) * N + nn] = t;
+        return;
+      }
       float v = alpha * t;
       if (bias) v += bias[nn];
       if (beta != 0.f) v += beta * C[mm * ldc + nn];
+      if (bn.on) v = bn_eval_apply(v, bn, nn);
       C[mm * ldc + nn] = v;
     }
   }
@@ -228,7 +254,7 @@ __global__ __launch_bounds__(kThreads) void linear_wgrad_kernel(const float* __r
 // C[m][n] = alpha * sum_z part[z][m][n] (+ bias[n]) + beta * C[m][n]   (fixed order)
 __global__ void gemm_splitk_reduce_kernel(const float* __restrict__ part, int splits, float* __restrict__ C,
                                           int64_t ldc, const float* __restrict__ bias, int M, int N, float alpha,
-                                          float beta) {
+                                          float beta, BnEv bn = BnEv{}) {
   const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;
   if (i >= (int64_t)M * N) return;
   const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
@@ -237,6 +263,7 @@ __global__ void gemm_splitk_reduce_kernel(const float* __restrict__ part, int sp
   float v = alpha * s;
   if (bias) v += bias[n];
   if (beta != 0.f) v += beta * C[m * ldc + n];
+  if (bn.on) v = bn_eval_apply(v, bn, n);
   C[m * ldc + n] = v;
 }
 
@@ -392,9 +419,34 @@ __global__ void act_bwd_kernel(const float* __restrict__ dy, const float* __rest
 
 }  // namespace
 
+namespace {
+int gemm_f32_impl(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn, float* C,
+                  int64_t ldc, const float* bias, int32_t M, int32_t N, int32_t K, float alpha, float beta,
+                  float* workspace, int64_t ws_floats, const BnEv& bn, void* stream);
+}  // namespace
+
 extern "C" int pose6d_gemm_f32(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
                                float* C, int64_t ldc, const float* bias, int32_t M, int32_t N, int32_t K, float alpha,
                                float beta, float* workspace, int64_t ws_floats, void* stream) {
+  return gemm_f32_impl(A, sam, sak, B, sbk, sbn, C, ldc, bias, M, N, K, alpha, beta, workspace, ws_floats, BnEv{},
+                       stream);
+}
+
+extern "C" int pose6d_gemm_f32_bn_eval(const float* A, int64_t sam, const float* W, float* C, int64_t ldc,
+                                       const float* bias, int32_t M, int32_t N, int32_t K, const float* gamma,
+                                       const float* beta, const float* running_mean, const float* running_var,
+                                       float eps, int32_t relu, float* workspace, int64_t ws_floats, void* stream) {
+  P6_CHECK_ARG(M > 0 && M <= 32 && N > 0 && K > 0, "pose6d_gemm_f32_bn_eval: batch must be 1..32 (skinny path)");
+  P6_CHECK_ARG(gamma && beta && running_mean && running_var, "pose6d_gemm_f32_bn_eval: null BatchNorm1d operand");
+  P6_CHECK_ARG(getenv("POSE6D_HEAD_GENERIC") == nullptr, "pose6d_gemm_f32_bn_eval: generic GEMM forced");
+  const BnEv bn{gamma, beta, running_mean, running_var, eps, relu != 0, 1};
+  return gemm_f32_impl(A, sam, 1, W, 1, K, C, ldc, bias, M, N, K, 1.f, 0.f, workspace, ws_floats, bn, stream);
+}
+
+namespace {
+int gemm_f32_impl(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn, float* C,
+                  int64_t ldc, const float* bias, int32_t M, int32_t N, int32_t K, float alpha, float beta,
+                  float* workspace, int64_t ws_floats, const BnEv& bn, void* stream) {
   P6_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "pose6d_gemm_f32: bad sizes");
   if (M == 0 || N == 0) return POSE6D_OK;
   hipStream_t s = p6::stream_of(stream);
@@ -403,21 +455,43 @@ extern "C" int pose6d_gemm_f32(const float* A, int64_t sam, int64_t sak, const f
   if (M <= 32 && sak == 1 && (bkc || bnc) && getenv("POSE6D_HEAD_GENERIC") == nullptr) {
     const bool vec = ((uintptr_t)A & 15) == 0 && (sam & 3) == 0 && (K & 3) == 0 &&
                      (!bkc || (((uintptr_t)B & 15) == 0 && (sbn & 3) == 0));
-    const dim3 grid(p6::ceil_div(N, 16));
+    // K slices: ~256 workgroups, each wave of a slice >= 16 deep (kSkW x 16 per slice),
+    // for weights of >= 4 MiB only: below that the reduce launch (~5 us) costs more than
+    // the slices save (1024 x 512: 8.6 us in one launch)
+    const int groups = p6::ceil_div(N, 16);
+    int slices = 1;
+    if (workspace && groups < 256 && (int64_t)N * K >= (1 << 20) && getenv("POSE6D_SKINNY_SPLIT") == nullptr) {
+      slices = p6::ceil_div(256, groups);
+      const int by_k = K / (kSkW * 16);
+      if (slices > by_k) slices = by_k;
+      const int64_t by_ws = ws_floats / ((int64_t)M * N);
+      if (slices > by_ws) slices = (int)by_ws;
+      if (slices < 1) slices = 1;
+    }
+    const int kchunk = slices > 1 ? p6::ceil_div(p6::ceil_div(K, slices), 16) * 16 : K;
+    slices = slices > 1 ? p6::ceil_div(K, kchunk) : 1;
+    float* part = slices > 1 ? workspace : nullptr;
+    const dim3 grid(groups, slices);
     if (bkc) {
       if (vec) skinny_gemm_kernel<true, true><<<grid, kSkThreads, 0, s>>>(A, sam, B, sbk, sbn, C, ldc, bias, M, N, K,
-                                                                          alpha, beta);
+                                                                          alpha, beta, kchunk, part, bn);
       else skinny_gemm_kernel<true, false><<<grid, kSkThreads, 0, s>>>(A, sam, B, sbk, sbn, C, ldc, bias, M, N, K,
-                                                                        alpha, beta);
+                                                                        alpha, beta, kchunk, part, bn);
     } else {
       if (vec) skinny_gemm_kernel<false, true><<<grid, kSkThreads, 0, s>>>(A, sam, B, sbk, sbn, C, ldc, bias, M, N, K,
-                                                                           alpha, beta);
+                                                                           alpha, beta, kchunk, part, bn);
       else skinny_gemm_kernel<false, false><<<grid, kSkThreads, 0, s>>>(A, sam, B, sbk, sbn, C, ldc, bias, M, N, K,
-                                                                         alpha, beta);
+                                                                         alpha, beta, kchunk, part, bn);
     }
     P6_LAUNCH_CHECK();
+    if (part) {
+      gemm_splitk_reduce_kernel<<<(unsigned)(((int64_t)M * N + kThreads - 1) / kThreads), kThreads, 0, s>>>(
+          part, slices, C, ldc, bias, M, N, alpha, beta, bn);
+      P6_LAUNCH_CHECK();
+    }
     return POSE6D_OK;
   }
+  P6_CHECK_ARG(!bn.on, "pose6d_gemm_f32_bn_eval: operands outside the skinny MFMA path (aligned, batch <= 32)");
   const int tiles = p6::ceil_div(N, TBN) * p6::ceil_div(M, TBM);
   // skinny (batch-32) GEMMs: split K so that >= ~256 workgroups stream the weights
   int splits = 1;
@@ -442,6 +516,7 @@ extern "C" int pose6d_gemm_f32(const float* A, int64_t sam, int64_t sak, const f
   }
   return POSE6D_OK;
 }
+}  // namespace
 
 extern "C" int pose6d_colsum_f32(const float* dy, int64_t ldy, float* db, int32_t M, int32_t N, int32_t accumulate,
                                  void* stream) {

@@ -9,6 +9,8 @@ Linear -> BatchNorm1d -> ReLU -> Dropout runs as 2 launches (GEMM + fused
 BN/ReLU/dropout column kernel), Linear -> LayerNorm -> GELU -> Dropout as 2
 (GEMM + fused row kernel); buffers are preallocated per batch size.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -116,8 +118,29 @@ class HeadEngine:
         st_ = stream()
         cur = x
         self.x = x
+        # eval without autograd: a Linear followed by an eval BatchNorm1d (no dropout)
+        # stores the normalised output directly (pose6d_gemm_f32_bn_eval, bit-identical
+        # to the two launches); nothing reads the Linear's raw output then
+        fuse_bn = (not training and not torch.is_grad_enabled() and B <= 32
+                   and os.environ.get("POSE6D_HEAD_BN_FUSE", "1") != "0")
+        skip = -1
         for i, st in enumerate(self.stages):
             st.x = cur
+            if i == skip:
+                cur = st.y
+                continue
+            nxt = self.stages[i + 1] if i + 1 < len(self.stages) else None
+            if (fuse_bn and st.kind == "linear" and nxt is not None and nxt.kind == "bn1d" and not nxt.mod.training
+                    and not (nxt.drop is not None and nxt.drop.training and nxt.drop.p > 0)):
+                m, bn = st.mod, nxt.mod
+                K, N = m.in_features, m.out_features
+                nxt.x, nxt.p, nxt.bn_train = st.y, 0.0, False
+                call("gemm_f32_bn_eval", cur, K, m.weight.detach(), nxt.y, N,
+                     m.bias.detach() if m.bias is not None else None, B, N, K, bn.weight.detach(), bn.bias.detach(),
+                     bn.running_mean, bn.running_var, float(bn.eps), nxt.act, self.ws, self.ws.numel(), st_)
+                skip = i + 1
+                cur = st.y
+                continue
             if st.kind == "linear":
                 m = st.mod
                 K, N = m.in_features, m.out_features

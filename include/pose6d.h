@@ -363,6 +363,16 @@ int pose6d_avgpool_bwd(int32_t dtype, const float *dy, void *dx, int32_t N, int3
 int pose6d_gemm_f32(const float *A, int64_t sam, int64_t sak, const float *B, int64_t sbk, int64_t sbn, float *C,
                     int64_t ldc, const float *bias, int32_t M, int32_t N, int32_t K, float alpha, float beta,
                     float *workspace, int64_t ws_floats, void *stream);
+/* eval-mode nn.Linear followed by nn.BatchNorm1d (running statistics) [+ ReLU], one
+ * launch path (replaces the rot/trans heads' Linear -> BatchNorm1d -> ReLU of
+ * pose_net_rgb.py:27-35 / pose_net_rgbd_geometric.py:28-38 at eval):
+ *   C[m][n] = act((A W^T + bias)[m][n] - rmean[n]) * (1 / sqrt(rvar[n] + eps)) * gamma[n] + beta[n])
+ * with pose6d_gemm_f32 + pose6d_bn1d_fwd(training = 0)'s arithmetic bit for bit.  A [M][sam]
+ * (K used), W [N][K] (nn.Linear weight), batch M <= 32. */
+int pose6d_gemm_f32_bn_eval(const float *A, int64_t sam, const float *W, float *C, int64_t ldc, const float *bias,
+                            int32_t M, int32_t N, int32_t K, const float *gamma, const float *beta,
+                            const float *running_mean, const float *running_var, float eps, int32_t relu,
+                            float *workspace, int64_t ws_floats, void *stream);
 /* nn.Linear parameter gradients in one launch: dW[n][k] (+)= sum_b dy[b*ldy + n] x[b*ldx + k],
  * db[n] (+)= sum_b dy[b*ldy + n] (db may be NULL); dW [N][K] contiguous. */
 int pose6d_linear_wgrad(const float *dy, int64_t ldy, const float *x, int64_t ldx, float *dw, float *db, int32_t N,

@@ -89,3 +89,29 @@ def test_eval_downsample_in_block_launch_is_bit_identical(dtype, monkeypatch):
         torch.cuda.synchronize()
     assert len(eng._dual_pairs()) == 8   # 4 blocks x (conv3, downsample)
     assert torch.equal(feats[0], feats[1])
+
+
+@pytest.mark.parametrize("name", list(EXPECTED))
+def test_eval_head_linear_bn1d_fused_is_bit_identical(name, monkeypatch):
+    """Eval heads: each Linear -> BatchNorm1d (+ ReLU) pair as one GEMM with the BN in
+    its store (pose6d_gemm_f32_bn_eval) equals the separate launches bit for bit,
+    with non-trivial running statistics."""
+    torch.manual_seed(0)
+    m = _models()[name](pretrained=False)
+    g = torch.Generator().manual_seed(13)
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.BatchNorm1d):
+            C = mod.num_features
+            mod.running_mean.copy_(torch.randn(C, generator=g) * 0.1)
+            mod.running_var.copy_(torch.rand(C, generator=g) + 0.5)
+            mod.weight.data.copy_(torch.rand(C, generator=g) + 0.5)
+    m = m.cuda().eval()
+    cin = {k: v.cuda() for k, v in _inputs(8, 224, g).items()}
+    outs = []
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("POSE6D_HEAD_BN_FUSE", fuse)
+        with torch.no_grad():
+            rot, trans = _model_forward(name, m, cin)
+        torch.cuda.synchronize()
+        outs.append((rot.clone(), trans.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
