@@ -657,7 +657,11 @@ template <typename T> struct LK { static constexpr int CH = 16 / (int)sizeof(T),
 
 // one workgroup's work; `bid_in` = its index in this conv's sub-grid (the whole grid,
 // or the leading part of a fused backward launch), `smem` = the kernel's dynamic LDS
-template <typename T, int BM, int BN, int MODE, int S, bool BNF = false, bool ACT = false, int NW = 4>
+// KG = 2 (small grids): two groups of NW waves share the tile; each stage holds two
+// K-steps, group g DMAs and multiplies the g-th, and the groups' sums meet in LDS
+// before the epilogue (group 1 then leaves) -- twice the waves per SIMD on grids of
+// about one workgroup per CU, where a lone wave cannot keep the MFMA pipe busy.
+template <typename T, int BM, int BN, int MODE, int S, bool BNF = false, bool ACT = false, int NW = 4, int KG = 1>
 __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* __restrict__ src,
                                               const T* __restrict__ wts, const float* __restrict__ bias,
                                               const T* __restrict__ res, T* __restrict__ out,
@@ -673,7 +677,10 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   static_assert(A_INS * RW == BM && B_INS * RW == BN, "tile rows must be a multiple of 8 x waves");
   constexpr int LOADS = A_INS + B_INS;
   constexpr int SA = BM * 128, STAGE = (BM + BN) * 128;
+  constexpr int STAGE_ALL = STAGE * KG;             // KG K-steps (slabs) per ring stage
   static_assert(S >= 2, "ring needs two stages");
+  static_assert(KG == 1 || (KG == 2 && NW == 4 && !BNF && (MODE == kGemm || MODE == kFwd)),
+                "K groups: 4-wave groups, plain forward only");
 
   const int per = g.gm * g.gn;
   const int nwg = MODE == kDgradS2 ? s2_classes(g) * per : per;
@@ -686,7 +693,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   // ids, so every XCD gets an even share of the heavy and the empty classes and the
   // four blocks that gather the same dY rows run on the same L2
   constexpr bool DUAL = MODE == kGemmDual;
-  int cls = -1, py = 0, px = 0, kh0 = 0, kw0 = 0, ntx = 1, nk = g.Kpad >> LOG_KS;
+  int cls = -1, py = 0, px = 0, kh0 = 0, kw0 = 0, ntx = 1, nk = (g.Kpad >> LOG_KS) / KG;
   const int nk1 = nk;   // kGemmDual: K-steps of the first (block) GEMM
   if (DUAL) nk += g.Kpad2 >> LOG_KS;
   if (MODE == kDgradS2) {
@@ -711,7 +718,9 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   if (g.nmajor) { tn = bid / g.gm; tm = bid - tn * g.gm; }
   else { tm = bid / g.gn; tn = bid - tm * g.gn; }
   const int m0 = tm * BM, n0 = tn * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((tid >> 6) & (NW - 1));   // wave within its K group
+  const int grp = KG > 1 ? __builtin_amdgcn_readfirstlane(tid >> 6) / NW : 0;
   const int wm = wave >> 1, wn = wave & 1;
   const int r8 = lane >> 3, pch = lane & 7;
   const char* zp = reinterpret_cast<const char*>(g_zero_page);
@@ -818,10 +827,11 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
 
   auto issue = [&](int kt, int buf) {
     (void)kt;
-    char* As = smem + buf * STAGE;
+    char* As = smem + buf * STAGE_ALL + grp * STAGE;   // group g fills slab g: K-step KG * stage + g
     char* Bs = As + SA;
     if (c0 == 0) set_tap();
-    const unsigned boff = (unsigned)(tap_koff + c0);
+    const int cg = c0 + grp * KS;
+    const unsigned boff = (unsigned)(tap_koff + cg);
 #pragma unroll
     for (int j = 0; j < B_INS; ++j) {
       const T* bb = b_base[j];
@@ -829,8 +839,8 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
       glds16(bb + (boff & b_mask[j]), Bs + (j * RW + wave * 8) * 128);
     }
 #pragma unroll
-    for (int i = 0; i < A_INS; ++i) glds16(a_base[i] + ((unsigned)c0 & a_mask[i]), As + (i * RW + wave * 8) * 128);
-    c0 += KS;
+    for (int i = 0; i < A_INS; ++i) glds16(a_base[i] + ((unsigned)cg & a_mask[i]), As + (i * RW + wave * 8) * 128);
+    c0 += KS * KG;
     if (c0 == tap_len) {
       c0 = 0;
       if constexpr (DUAL) {
@@ -876,7 +886,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   // mid(): issued between the fragment reads and their wait, so the next stage's
   // LDS-DMA issue (tens of cycles per instruction) overlaps the LDS read latency
   auto compute = [&](int buf, auto&& mid, auto& acc) {
-    const unsigned slot = ring_base + buf * STAGE;
+    const unsigned slot = ring_base + buf * STAGE_ALL + grp * STAGE;
     if constexpr (TM + TN == 4 && kPairedFrags) {
       unsigned addr[2][4];
 #pragma unroll
@@ -939,6 +949,29 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
     wbuf = wbuf == S - 1 ? 0 : wbuf + 1;
   }
   asm volatile("s_barrier" ::: "memory");   // every wave done reading the ring before the epilogue reuses it
+  if constexpr (KG == 2) {
+    // group 1's sums -> LDS (past the epilogue's staging area) -> added by group 0 in
+    // the same (wave, lane, tile) slots; group 1 then joins the epilogue's one barrier
+    // and leaves (no store of its own)
+    constexpr int RED = STAGE_ALL;   // offset: the second half of the 2-stage ring
+    static_assert(RED >= BM * (BN * (int)sizeof(T) + 16), "reduction area overlaps the epilogue staging");
+    f32x4* red = reinterpret_cast<f32x4*>(smem + RED);
+    if (grp == 1) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) red[((wave * TM + i) * TN + j) * 64 + lane] = acc[i][j];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (grp == 1) {
+      asm volatile("s_barrier" ::: "memory");   // pairs with the epilogue's staging barrier
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] += red[((wave * TM + i) * TN + j) * 64 + lane];
+  }
   if constexpr (DUAL)   // acc2 = the block GEMM, acc = the downsample branch
     conv_epilogue<T, BM, BN, false, 1, NW, true>(acc2, smem, g, bias, nullptr, out, nullptr, m0, n0, -1, nullptr, 0,
                                                  acc);
@@ -947,13 +980,13 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
                                                    MODE == kDgradS2 ? tm * 4 + cls : tm);
 }
 
-template <typename T, int BM, int BN, int MODE, int S, bool ACT, int NW>
-__global__ __launch_bounds__(64 * NW) void conv_lds_kernel(const T* __restrict__ src, const T* __restrict__ wts,
-                                                           const float* __restrict__ bias,
-                                                           const T* __restrict__ res, T* __restrict__ out,
-                                                           float* __restrict__ stats, Geom g) {
+template <typename T, int BM, int BN, int MODE, int S, bool ACT, int NW, int KG = 1>
+__global__ __launch_bounds__(64 * NW * KG) void conv_lds_kernel(const T* __restrict__ src, const T* __restrict__ wts,
+                                                                const float* __restrict__ bias,
+                                                                const T* __restrict__ res, T* __restrict__ out,
+                                                                float* __restrict__ stats, Geom g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv_lds_body<T, BM, BN, MODE, S, false, ACT, NW>(smem, blockIdx.x, src, wts, bias, res, out, stats, g);
+  conv_lds_body<T, BM, BN, MODE, S, false, ACT, NW, KG>(smem, blockIdx.x, src, wts, bias, res, out, stats, g);
 }
 
 // Fused backward of one conv: workgroups [0, nd) compute the data gradient,
@@ -1001,14 +1034,15 @@ int stage_bytes(int tile) {
   return (bm[tile] + bn[tile]) * 128;
 }
 
-template <typename T, int BM, int BN, int MODE, int S, int NW = 4>
+template <typename T, int BM, int BN, int MODE, int S, int NW = 4, int KG = 1>
 int launch_fast(const Geom& g0, const void* src, const void* w, const float* bias, const void* res, void* out,
                 float* stats, hipStream_t s) {
   Geom g = g0;
   g.gm = p6::ceil_div(g.M, BM);
   g.gn = p6::ceil_div(g.Ncols, BN);
-  const int nk = fast_nk(MODE, g, LK<T>::KS);
-  const int ring = (nk < S ? (nk > 0 ? nk : 1) : S) * (BM + BN) * 128;
+  const int nk = fast_nk(MODE, g, LK<T>::KS) / KG;
+  // K groups: the whole S-stage ring (the reduction area is its second stage)
+  const int ring = (KG > 1 ? S : (nk < S ? (nk > 0 ? nk : 1) : S)) * (BM + BN) * 128 * KG;
   // kGemmDual stages both branches' tiles for its epilogue
   const int epi = (MODE == kGemmDual ? 2 : 1) * BM * (BN * (int)sizeof(T) + 16);
   const int lds = ring > epi ? ring : epi;
@@ -1016,14 +1050,14 @@ int launch_fast(const Geom& g0, const void* src, const void* w, const float* bia
   const int grid = g.gm * g.gn * (MODE == kDgradS2 ? s2_classes(g) : 1);
   if constexpr (MODE == kGemm || MODE == kFwd || MODE == kGemmDual) {
     if (g.act) {   // eval BN-act epilogue (pose6d_conv2d_fwd_act)
-      conv_lds_kernel<T, BM, BN, MODE, S, true, NW><<<grid, 64 * NW, lds, s>>>((const T*)src, (const T*)w, bias,
-                                                                               (const T*)res, (T*)out, stats, g);
+      conv_lds_kernel<T, BM, BN, MODE, S, true, NW, KG><<<grid, 64 * NW * KG, lds, s>>>(
+          (const T*)src, (const T*)w, bias, (const T*)res, (T*)out, stats, g);
       P6_LAUNCH_CHECK();
       return POSE6D_OK;
     }
   }
-  conv_lds_kernel<T, BM, BN, MODE, S, false, NW><<<grid, 64 * NW, lds, s>>>((const T*)src, (const T*)w, bias,
-                                                                             (const T*)res, (T*)out, stats, g);
+  conv_lds_kernel<T, BM, BN, MODE, S, false, NW, KG><<<grid, 64 * NW * KG, lds, s>>>(
+      (const T*)src, (const T*)w, bias, (const T*)res, (T*)out, stats, g);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
@@ -1050,6 +1084,10 @@ int launch_fast_mode(const Geom& g, int tile, int stages, const void* src, const
     case 1: return launch_fast_s<T, 128, 64, MODE>(g, stages, src, w, bias, res, out, stats, s);
     case 4: return launch_fast_s<T, 128, 128, MODE, 8>(g, stages, src, w, bias, res, out, stats, s);
     case 5: return launch_fast_s<T, 128, 64, MODE, 8>(g, stages, src, w, bias, res, out, stats, s);
+    case 6:   // 64x64, two K groups of 4 waves (2 ring stages of 2 K-steps)
+      if constexpr (MODE == kGemm || MODE == kFwd) return launch_fast<T, 64, 64, MODE, 2, 4, 2>(g, src, w, bias, res,
+                                                                                               out, stats, s);
+      else return p6::set_error(POSE6D_EINVAL, "conv: K-group tile for a forward mode only");
     default: return launch_fast_s<T, 64, 64, MODE>(g, stages, src, w, bias, res, out, stats, s);
   }
 }
@@ -1215,8 +1253,27 @@ Plan choose(int dtype, int mode, const Geom& g, bool fused = false) {
     const char* ord = getenv("POSE6D_CONV_ORDER");
     p.g.nmajor = ord && ord[0] == 'n';
   }
-  p.tile = (fused || mode == kGemmDual) ? 3 : env_int("POSE6D_CONV_TILE", pick_tile_fast(dtype, p.g.M, g.Ncols, g.K));
+  int dflt_tile = pick_tile_fast(dtype, p.g.M, g.Ncols, g.K);
+  // (never the 1x1 stride-2 downsample convs: their eval output must keep the summation
+  // order of the one-launch block kernel, pose6d_conv2d_fwd_act_dual, bit for bit)
+  if (dflt_tile == 3 && dtype == POSE6D_DT_BF16 && (p.mode == kGemm || p.mode == kFwd) &&
+      !(g.KH == 1 && g.stride == 2) && env_int("POSE6D_CONV_KG", 0)) {
+    // two K groups per 64x64 tile where a grid of ~1.5 workgroups per CU leaves the
+    // waves alone on their SIMDs: opt-in (POSE6D_CONV_KG=1).  Graph-timed single convs
+    // (profiles/r02c_conv_kgroups.txt) put layer3's 3x3 / 1x1-reduce 9-11 % and layer4's
+    // 1x1-reduce 9 % faster, but inside the eval forward graph it lost on one box,
+    // A/B alternated: 0.991 vs 0.981 ms (profiles/r02c_ab_kgroups.txt)
+    const int64_t g64 = (int64_t)p6::ceil_div(p.g.M, 64) * p6::ceil_div(g.Ncols, 64);
+    if ((g64 >= 300 && g64 <= 450) || (p.mode == kGemm && g64 <= 256 && g.K >= 2048)) dflt_tile = 6;
+  }
+  p.tile = (fused || mode == kGemmDual) ? 3 : env_int("POSE6D_CONV_TILE", dflt_tile);
   if (p.tile == 2) p.tile = 3;   // no 64x128 instance on the fast path
+  if (p.tile == 6) {
+    // K groups: forward modes whose K-steps pair up inside every filter tap
+    const int ks = dtype == POSE6D_DT_BF16 ? 64 : 32;
+    const int tap_len = p.mode == kGemm ? g.Kpad : g.SC;
+    if (!(p.mode == kGemm || p.mode == kFwd) || tap_len % (2 * ks) != 0) p.tile = 3;
+  }
   // two slots (32 KiB at 64x64) keep several workgroups per CU resident, which hides
   // the DMA latency better than a deeper ring; only long-K grids that leave CUs
   // idle (one wave of workgroups) take a 4-deep ring

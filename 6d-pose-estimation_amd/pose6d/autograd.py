@@ -31,9 +31,12 @@ class _EngineFn(torch.autograd.Function):
         return (dx, None, None, None) + tuple(grads[id(p)] for p in ctx.params)
 
 
-def run(eng, x, training, params, **extra):
-    """Apply an engine with autograd when gradients are needed."""
+def run(eng, x, training, params, copy=True, **extra):
+    """Apply an engine with autograd when gradients are needed.  Without autograd the
+    engine's output buffer is returned as is when copy=False (the caller consumes it
+    before the engine runs again: trunk features feeding the heads)."""
     params = [p for p in params]
     if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params)):
         return _EngineFn.apply(x, eng, training, extra, *params)
-    return eng.forward(x, training, **extra).clone()
+    out = eng.forward(x, training, **extra)
+    return out.clone() if copy else out

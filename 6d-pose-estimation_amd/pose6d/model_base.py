@@ -47,7 +47,8 @@ class EngineModel(nn.Module):
     def _run_trunk(self, name, seq, x, in_channels, kind="resnet50"):
         eng = self._engine(name, lambda: TrunkEngine(seq, in_channels, kind))
         eng.set_dtype(self._p6_dtype)
-        return autograd.run(eng, x, self.training, list(seq.parameters()))
+        # trunk features only ever feed the model's own heads / fusion: no copy
+        return autograd.run(eng, x, self.training, list(seq.parameters()), copy=False)
 
     def _run_head(self, name, seq, x, salt):
         eng = self._engine(name, lambda: HeadEngine(seq))

@@ -399,3 +399,58 @@ def test_pack_layouts(dtype, O, I, k, cpad):
     assert torch.equal(wp.float(), full.to(dtype).float())
     if I >= 8:
         assert torch.equal(wt.float(), w.permute(1, 2, 3, 0).to(dtype).float())
+
+
+KG_CONFIGS = [
+    # N, H, W, Cin, Cout, k, s, p: K-steps pair up inside every tap (Cin % 128 for bf16)
+    (2, 14, 14, 128, 128, 1, 1, 0),
+    (2, 14, 14, 128, 64, 3, 1, 1),
+    (2, 28, 28, 256, 128, 3, 2, 1),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cfg", KG_CONFIGS)
+def test_conv_fwd_kgroup_tile(cfg, dtype, monkeypatch):
+    """The two-K-group 64x64 tile (POSE6D_CONV_TILE=6; group 1's sums added to group
+    0's in LDS) against the torch fp32 conv, its BN statistics against the batch
+    moments, and its eval BN-act store against y * scale + shift -> ReLU."""
+    from pose6d._lib import call, query, stream
+    from pose6d.trunk import DTYPES, pack_single
+    monkeypatch.setenv("POSE6D_CONV_TILE", "6")
+    N, H, W, Cin, Cout, k, s, p = cfg
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, k, k, generator=g) * (2.0 / (Cin * k * k)) ** 0.5
+    if dtype == torch.bfloat16:
+        x = x.bfloat16().float()
+        w = w.bfloat16().float()
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dt, dev = DTYPES[dtype], "cuda"
+    xd = _nhwc(x).to(dev, dtype)
+    wp, _ = pack_single(w.to(dev), Cin, dtype, with_t=False)
+    y = torch.empty(N, Ho, Wo, Cout, device=dev, dtype=dtype)
+    rows = query("conv_stats_rows", N, Ho, Wo, Cout)
+    stats = torch.empty(2, Cout, rows, device=dev)
+    call("conv2d_fwd", dt, xd, wp, None, y, stats, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream())
+    yr = F.conv2d(x, w, None, stride=s, padding=p)
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    _close(y.permute(0, 3, 1, 2), yr, tol, "fwd (K groups)")
+    C = Cout
+    one, zero = torch.ones(C, device=dev), torch.zeros(C, device=dev)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    sc, sh, mu, iv = (torch.empty(C, device=dev) for _ in range(4))
+    ws = torch.empty(64 * 3 * C, device=dev, dtype=torch.float64)
+    call("bn_finalize", stats, rows, C, N * Ho * Wo, one, zero, rm, rv, None, 0.1, 1e-5, 1, sc, sh, mu, iv, ws,
+         stream())
+    _close(mu, yr.double().mean((0, 2, 3)), 1e-4 if dtype == torch.float32 else 1e-2, "batch mean (K groups)")
+    scale = torch.rand(C, device=dev) + 0.5
+    shift = torch.randn(C, device=dev) * 0.1
+    out = torch.empty_like(y)
+    call("conv2d_fwd_act", dt, xd, wp, None, out, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, scale, shift, None, None,
+         None, 1, stream())
+    ref = torch.empty_like(y)   # the separate BN-act launch on the stored conv output
+    call("bn_act_fwd", dt, y, scale, shift, None, None, None, 1, ref, N * Ho * Wo, Cout, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
