@@ -342,11 +342,23 @@ def rgb_fp32_forward(dev, B=32, reps=10):
     m = PoseNetRGB(pretrained=False).to(dev).set_compute_dtype(torch.float32).eval()
     x = torch.randn(B, 3, 224, 224, device=dev)
     with torch.no_grad():
-        t = _time_fn(lambda: m(x), reps)
+        t_eager = _time_fn(lambda: m(x), reps)
+        # the same forward captured once into a hipGraph and replayed (as the eval
+        # forward_roofline_eval line): the GPU-side rate without host launch gaps
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            m(x)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            m(x)
+        t = _time_fn(g.replay, reps)
     gbs = FWD_BYTES_PER_CROP_F32 * B / t / 1e9
     tf = RGB_FWD_FLOPS_PER_CROP * B / t / 1e12
-    return {"workload": "PoseNetRGB forward, eval mode, bs32 224^2, fp32", "value": round(B / t, 1),
-            "unit": "crops/s", "ms_per_batch": round(t * 1e3, 4), "dtype": "f32",
+    return {"workload": "PoseNetRGB forward, eval mode, bs32 224^2, fp32 (hipGraph replay; eager beside it)",
+            "value": round(B / t, 1), "unit": "crops/s", "ms_per_batch": round(t * 1e3, 4),
+            "eager_ms_per_batch": round(t_eager * 1e3, 4), "dtype": "f32",
             "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(tf / PEAK_F32_MFMA_TFLOPS, 4),
                          "algorithmic_flops_per_crop": RGB_FWD_FLOPS_PER_CROP},
