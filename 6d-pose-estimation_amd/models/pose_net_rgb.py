@@ -36,7 +36,7 @@ class PoseNetRGB(EngineModel):
     def forward(self, x):
         """RGB image -> (rotation, translation) (pose_net_rgb.py:56-65)."""
         features = self._run_trunk("backbone", self.backbone, x, 3)
-        rotation = ops.normalize(self._run_head("rot_head", self.rot_head, features, salt=1))
+        rotation = ops.normalize(self._run_head("rot_head", self.rot_head, features, salt=1, copy=False))
         translation = self._run_head("trans_head", self.trans_head, features, salt=2)
         self._advance_seed()
         return rotation, translation

@@ -41,7 +41,7 @@ class PoseNetRGBGeometric(EngineModel):
     def forward(self, rgb, bbox_center=None, camera_matrix=None):
         """pose_net_rgb_geometric.py:70-91."""
         rgb_features = self._run_trunk("rgb_backbone", self.rgb_backbone, rgb, 3)
-        rotation = ops.normalize_eps(self._run_head("rot_head", self.rot_head, rgb_features, salt=1))
+        rotation = ops.normalize_eps(self._run_head("rot_head", self.rot_head, rgb_features, salt=1, copy=False))
         z_features = self._run_trunk("z_backbone", self.z_backbone, rgb, 3, kind="zcnn")
         z_pred = self._run_head("z_predictor", self.z_predictor, z_features, salt=2)
         self._advance_seed()

@@ -96,7 +96,7 @@ class PoseNetRGBD(EngineModel):
                                                                       self.depth_norm))
         combined = fusion.run(eng, rgb_feat, depth_feat, self.training, seed_dev=self._p6_seed, salt=3)
         fused = self._run_head("fusion", self.fusion, combined, salt=4)
-        rotation = ops.normalize(self._run_head("rot_head", self.rot_head, fused, salt=5))
+        rotation = ops.normalize(self._run_head("rot_head", self.rot_head, fused, salt=5, copy=False))
         translation = self._run_head("trans_head", self.trans_head, fused, salt=6)
         self._advance_seed()
         return rotation, translation

@@ -31,7 +31,7 @@ class PoseNetRGBDGeometric(EngineModel):
     def forward(self, rgb, depth=None, depth_raw=None, bbox_center=None, camera_matrix=None):
         """RGB -> rotation; depth sensor -> translation (pose_net_rgbd_geometric.py:40-54)."""
         features = self._run_trunk("backbone", self.backbone, rgb, 3)
-        rotation = ops.normalize(self._run_head("rot_head", self.rot_head, features, salt=1))
+        rotation = ops.normalize(self._run_head("rot_head", self.rot_head, features, salt=1, copy=False))
         self._advance_seed()
         if depth_raw is not None and bbox_center is not None and camera_matrix is not None:
             translation = self._compute_pinhole_translation(depth_raw, bbox_center, camera_matrix)

@@ -50,9 +50,12 @@ class EngineModel(nn.Module):
         # trunk features only ever feed the model's own heads / fusion: no copy
         return autograd.run(eng, x, self.training, list(seq.parameters()), copy=False)
 
-    def _run_head(self, name, seq, x, salt):
+    def _run_head(self, name, seq, x, salt, copy=True):
+        """copy=False: the output is consumed right away by another op (normalize,
+        pinhole) and never reaches the caller, so no-grad forwards skip the copy."""
         eng = self._engine(name, lambda: HeadEngine(seq))
-        return autograd.run(eng, x, self.training, list(seq.parameters()), seed_dev=self._p6_seed, salt=salt)
+        return autograd.run(eng, x, self.training, list(seq.parameters()), copy=copy, seed_dev=self._p6_seed,
+                            salt=salt)
 
     def _advance_seed(self):
         if self.training:
