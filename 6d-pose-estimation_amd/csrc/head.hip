@@ -283,6 +283,7 @@ using p6::uniform01;
 // per lane: coalesced rows) x 4 row groups (one per wave, rows g, g+4, ...); the
 // per-group fp64 sums meet in LDS and are combined in group order (deterministic).
 constexpr int kBnCols = 64, kBnGroups = kThreads / kBnCols;
+constexpr int kRU = 8;   // rows per apply trip (batch 32 = one trip of 4 groups x 8)
 
 __device__ __forceinline__ double group_total(double v, double (*red)[kBnCols], int g, int cl) {
   red[g][cl] = v;
@@ -330,16 +331,30 @@ __global__ __launch_bounds__(kThreads) void bn1d_fwd_kernel(
   }
   const float gm = gamma[c], b = beta[c];
   const float keep_scale = p_drop > 0.f ? 1.0f / (1.0f - p_drop) : 1.0f;
-  for (int m = g; m < M; m += kBnGroups) {
-    const int64_t o = (int64_t)m * C + c;
-    float v = (x[o] - mean) * inv * gm + b;
-    if (relu) v = fmaxf(v, 0.f);
-    if (p_drop > 0.f) {
-      const bool keep = uniform01(seedp[0] ^ salt, (uint64_t)o) >= p_drop;
-      mask[o] = keep;
-      v = keep ? v * keep_scale : 0.f;
+  const uint64_t seed = p_drop > 0.f ? seedp[0] ^ salt : 0;
+  // kRU rows per trip, every load before the trip's stores (a load issued behind a
+  // store waits for the store's acknowledgement)
+  for (int m0 = g; m0 < M; m0 += kRU * kBnGroups) {
+    float v[kRU];
+#pragma unroll
+    for (int u = 0; u < kRU; ++u) {
+      const int m = m0 + u * kBnGroups;
+      v[u] = m < M ? x[(int64_t)m * C + c] : 0.f;
     }
-    y[o] = v;
+#pragma unroll
+    for (int u = 0; u < kRU; ++u) {
+      const int m = m0 + u * kBnGroups;
+      if (m >= M) break;
+      const int64_t o = (int64_t)m * C + c;
+      float t = (v[u] - mean) * inv * gm + b;
+      if (relu) t = fmaxf(t, 0.f);
+      if (p_drop > 0.f) {
+        const bool keep = uniform01(seed, (uint64_t)o) >= p_drop;
+        mask[o] = keep;
+        t = keep ? t * keep_scale : 0.f;
+      }
+      y[o] = t;
+    }
   }
 }
 
@@ -377,11 +392,22 @@ __global__ __launch_bounds__(kThreads) void bn1d_bwd_kernel(
     if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + (float)sd;
   }
   const float c2 = (float)(sd / M), c3 = (float)(sdx / M);
-  for (int m = g; m < M; m += kBnGroups) {
-    const int64_t o = (int64_t)m * C + c;
-    const float d = grad_in(o);
-    const float xh = (x[o] - mean) * inv;
-    dx[o] = training ? gm * inv * (d - c2 - xh * c3) : gm * inv * d;
+  for (int m0 = g; m0 < M; m0 += kRU * kBnGroups) {   // loads of a trip before its stores
+    float dv[kRU], xv[kRU];
+#pragma unroll
+    for (int u = 0; u < kRU; ++u) {
+      const int m = m0 + u * kBnGroups;
+      const int64_t o = (int64_t)(m < M ? m : m0) * C + c;
+      dv[u] = grad_in(o);
+      xv[u] = x[o];
+    }
+#pragma unroll
+    for (int u = 0; u < kRU; ++u) {
+      const int m = m0 + u * kBnGroups;
+      if (m >= M) break;
+      const float xh = (xv[u] - mean) * inv;
+      dx[(int64_t)m * C + c] = training ? gm * inv * (dv[u] - c2 - xh * c3) : gm * inv * dv[u];
+    }
   }
 }
 
