@@ -8,6 +8,8 @@
 //                            backward gathers in output order (deterministic);
 //                            one lane per (pixel, 16-byte channel chunk)
 //   pose6d_avgpool_fwd/bwd   nn.AdaptiveAvgPool2d(1) + view(B, -1)
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -166,63 +168,20 @@ __global__ __launch_bounds__(kThreads) void pack_kernel(const PackDesc* __restri
   }
 }
 
-template <typename T>
-__global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ idx, int N, int H,
-                                   int W, int C, int Ho, int Wo, int k, int s, int p) {
+// One lane per (output pixel, 16-byte channel chunk).  BN: the window
+// element is T(max(y * scale + shift, 0)), exactly what pose6d_bn_act_fwd would have
+// stored (the stem / z-CNN act -> pool pairs), so the pooled values and argmax equal
+// bn_act_fwd followed by maxpool_fwd bit for bit -- without writing and re-reading the
+// full-resolution activation (nothing else reads it: the backward recomputes the ReLU
+// sign from y and routes the pool gradient by argmax).
+template <typename T, bool BN>
+__global__ __launch_bounds__(kThreads) void pool_fwd_kernel(const T* __restrict__ x, const float* __restrict__ scale,
+                                                            const float* __restrict__ shift, T* __restrict__ y,
+                                                            uint8_t* __restrict__ idx, int N, int H, int W, int C,
+                                                            int Ho, int Wo, int k, int s, int p) {
   constexpr int E = V<T>::E;
   const int cpr = C / E;
   // grid (ceil(Wo * cpr / 256), N * Ho): one output row per blockIdx.y
-  const int i = blockIdx.x * kThreads + threadIdx.x;  // (column, chunk) within the row
-  if (i >= Wo * cpr) return;
-  const int n = blockIdx.y / Ho, oy = blockIdx.y - n * Ho;
-  const int ox = i / cpr, c0 = (i - ox * cpr) * E;
-  const int64_t pix = ((int64_t)n * Ho + oy) * Wo + ox;
-  float best[E];
-  uint8_t bi[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) { best[e] = -__builtin_inff(); bi[e] = 0; }
-  bool first = true;
-  for (int kh = 0; kh < k; ++kh) {
-    const int iy = oy * s - p + kh;
-    if (iy < 0 || iy >= H) continue;
-    for (int kw = 0; kw < k; ++kw) {
-      const int ix = ox * s - p + kw;
-      if (ix < 0 || ix >= W) continue;
-      float v[E];
-      ld(x + (((int64_t)n * H + iy) * W + ix) * C + c0, v);
-#pragma unroll
-      for (int e = 0; e < E; ++e)
-        if (first || v[e] > best[e] || v[e] != v[e]) { best[e] = v[e]; bi[e] = (uint8_t)(kh * k + kw); }
-      first = false;
-    }
-  }
-  st(y + pix * C + c0, best);
-  if (idx) {
-    if constexpr (E == 8) {
-      uint2 u;
-      __builtin_memcpy(&u, bi, 8);
-      *reinterpret_cast<uint2*>(idx + pix * C + c0) = u;
-    } else {
-      uint32_t u;
-      __builtin_memcpy(&u, bi, 4);
-      *reinterpret_cast<uint32_t*>(idx + pix * C + c0) = u;
-    }
-  }
-}
-
-// BatchNorm-apply + ReLU + max pool in one pass (the stem / z-CNN act -> pool pairs):
-// the pool reads the raw conv output y and forms each window element exactly as
-// pose6d_bn_act_fwd would have stored it, T(max(y * scale + shift, 0)), so the pooled
-// values and argmax equal bn_act_fwd followed by maxpool_fwd bit for bit -- without
-// writing and re-reading the full-resolution activation (nothing else reads it: the
-// backward recomputes the ReLU sign from y and routes the pool gradient by argmax).
-template <typename T>
-__global__ void bn_relu_maxpool_fwd_kernel(const T* __restrict__ x, const float* __restrict__ scale,
-                                           const float* __restrict__ shift, T* __restrict__ y,
-                                           uint8_t* __restrict__ idx, int N, int H, int W, int C, int Ho, int Wo,
-                                           int k, int s, int p) {
-  constexpr int E = V<T>::E;
-  const int cpr = C / E;
   const int i = blockIdx.x * kThreads + threadIdx.x;  // (column, chunk) within the output row
   if (i >= Wo * cpr) return;
   const int n = blockIdx.y / Ho, oy = blockIdx.y - n * Ho;
@@ -232,12 +191,24 @@ __global__ void bn_relu_maxpool_fwd_kernel(const T* __restrict__ x, const float*
   uint8_t bi[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
-    sc[e] = scale[c0 + e];
-    sh[e] = shift[c0 + e];
+    if constexpr (BN) {
+      sc[e] = scale[c0 + e];
+      sh[e] = shift[c0 + e];
+    }
     best[e] = -__builtin_inff();
     bi[e] = 0;
   }
   bool first = true;
+  auto take = [&](const float* raw, int j) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      float v = raw[e];
+      if constexpr (BN) v = p6::to_f(p6::from_f<T>(fmaxf(fmaf(v, sc[e], sh[e]), 0.f)));
+      if (first || v > best[e] || v != v) { best[e] = v; bi[e] = (uint8_t)j; }
+    }
+    first = false;
+  };
+  const T* xn = x + (int64_t)n * H * W * C + c0;
   for (int kh = 0; kh < k; ++kh) {
     const int iy = oy * s - p + kh;
     if (iy < 0 || iy >= H) continue;
@@ -245,13 +216,8 @@ __global__ void bn_relu_maxpool_fwd_kernel(const T* __restrict__ x, const float*
       const int ix = ox * s - p + kw;
       if (ix < 0 || ix >= W) continue;
       float v[E];
-      ld(x + (((int64_t)n * H + iy) * W + ix) * C + c0, v);
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        v[e] = p6::to_f(p6::from_f<T>(fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f)));
-        if (first || v[e] > best[e] || v[e] != v[e]) { best[e] = v[e]; bi[e] = (uint8_t)(kh * k + kw); }
-      }
-      first = false;
+      ld(xn + ((int64_t)iy * W + ix) * C, v);
+      take(v, kh * k + kw);
     }
   }
   st(y + pix * C + c0, best);
@@ -268,10 +234,22 @@ __global__ void bn_relu_maxpool_fwd_kernel(const T* __restrict__ x, const float*
   }
 }
 
-template <typename T>
-__global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx, T* __restrict__ dx, int N,
-                                   int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
+template <typename T, bool BN>
+void launch_pool_fwd(dim3 grid, hipStream_t st_, const T* x, const float* scale, const float* shift, T* y,
+                     uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
+  pool_fwd_kernel<T, BN><<<grid, kThreads, 0, st_>>>(x, scale, shift, y, idx, N, H, W, C, Ho, Wo, k, s, p);
+}
+
+// NW > 0: at most NW windows per axis contain an input pixel (ceil(k / s) <= NW: 2 for
+// the 3x3 / s2 stem pool, 1 for the z-CNN 2x2 / s2 pools); all NW * NW candidate dy / argmax
+// loads are issued up front (out-of-range candidates read a clamped in-range window and
+// are skipped), then summed in the same (oy, ox) order as the generic loop -- bit-identical.
+template <typename T, int NW>
+__global__ __launch_bounds__(kThreads) void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                               T* __restrict__ dx, int N, int H, int W, int C, int Ho,
+                                                               int Wo, int k, int s, int p) {
   constexpr int E = V<T>::E;
+  using IdxVec = typename std::conditional<E == 8, uint2, uint32_t>::type;
   const int cpr = C / E;
   // grid (ceil(W * cpr / 256), N * H): one input row per blockIdx.y
   const int i = blockIdx.x * kThreads + threadIdx.x;  // (column, chunk) within the row
@@ -285,21 +263,63 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __re
   float g[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) g[e] = 0.f;
-  for (int oy = oy0; oy <= oy1; ++oy)
-    for (int ox = ox0; ox <= ox1; ++ox) {
-      const int kh = iy - (oy * s - p), kw = ix - (ox * s - p);
-      if (kh < 0 || kw < 0 || kh >= k || kw >= k) continue;
-      const uint8_t me = (uint8_t)(kh * k + kw);
-      const int64_t o = (((int64_t)n * Ho + oy) * Wo + ox) * C + c0;
-      uint8_t bi[E];
-      __builtin_memcpy(bi, idx + o, E);
-      float d[E];
-      ld(dy + o, d);
+  auto add = [&](const uint4& draw, IdxVec iraw, uint8_t me) {
+    uint8_t bi[E];
+    __builtin_memcpy(bi, &iraw, E);
+    T t[E];
+    __builtin_memcpy(t, &draw, 16);
 #pragma unroll
-      for (int e = 0; e < E; ++e)
-        if (bi[e] == me) g[e] += d[e];
+    for (int e = 0; e < E; ++e)
+      if (bi[e] == me) g[e] += p6::to_f(t[e]);
+  };
+  const int64_t nbase = (int64_t)n * Ho * Wo * C + c0;
+  if constexpr (NW > 0) {
+    uint4 draw[NW * NW];
+    IdxVec iraw[NW * NW];
+    uint8_t me[NW * NW];
+    bool ok[NW * NW];
+#pragma unroll
+    for (int a = 0; a < NW; ++a) {
+      const int oy = oy0 + a;
+      const int cy = oy < Ho ? oy : Ho - 1;
+#pragma unroll
+      for (int b = 0; b < NW; ++b) {
+        const int ox = ox0 + b;
+        const int cx = ox < Wo ? ox : Wo - 1;
+        const int kh = iy - (oy * s - p), kw = ix - (ox * s - p);
+        const int j = a * NW + b;
+        ok[j] = oy <= oy1 && ox <= ox1 && kh >= 0 && kw >= 0 && kh < k && kw < k;
+        me[j] = (uint8_t)(kh * k + kw);
+        const int64_t o = nbase + ((int64_t)cy * Wo + cx) * C;
+        draw[j] = *reinterpret_cast<const uint4*>(dy + o);
+        iraw[j] = *reinterpret_cast<const IdxVec*>(idx + o);
+      }
     }
+#pragma unroll
+    for (int j = 0; j < NW * NW; ++j)
+      if (ok[j]) add(draw[j], iraw[j], me[j]);
+  } else {
+    for (int oy = oy0; oy <= oy1; ++oy)
+      for (int ox = ox0; ox <= ox1; ++ox) {
+        const int kh = iy - (oy * s - p), kw = ix - (ox * s - p);
+        if (kh < 0 || kw < 0 || kh >= k || kw >= k) continue;
+        const int64_t o = nbase + ((int64_t)oy * Wo + ox) * C;
+        add(*reinterpret_cast<const uint4*>(dy + o), *reinterpret_cast<const IdxVec*>(idx + o),
+            (uint8_t)(kh * k + kw));
+      }
+  }
   st(dx + pix * C + c0, g);
+}
+
+template <typename T>
+void launch_pool_bwd(int nw, dim3 grid, hipStream_t st_, const T* dy, const uint8_t* idx, T* dx, int N, int H, int W,
+                     int C, int Ho, int Wo, int k, int s, int p) {
+  if (nw <= 1)
+    maxpool_bwd_kernel<T, 1><<<grid, kThreads, 0, st_>>>(dy, idx, dx, N, H, W, C, Ho, Wo, k, s, p);
+  else if (nw == 2)
+    maxpool_bwd_kernel<T, 2><<<grid, kThreads, 0, st_>>>(dy, idx, dx, N, H, W, C, Ho, Wo, k, s, p);
+  else
+    maxpool_bwd_kernel<T, 0><<<grid, kThreads, 0, st_>>>(dy, idx, dx, N, H, W, C, Ho, Wo, k, s, p);
 }
 
 // block = 64 channel chunks (lanes) x 4 pixel groups (waves), grid (chunk groups, N);
@@ -409,10 +429,11 @@ extern "C" int pose6d_maxpool_fwd(int32_t dtype, const void* x, void* y, uint8_t
   const int E = dtype == POSE6D_DT_BF16 ? 8 : 4;
   const dim3 grid(p6::ceil_div((int64_t)Wo * (C / E), kThreads), N * Ho);
   if (dtype == POSE6D_DT_BF16)
-    maxpool_fwd_kernel<bf16><<<grid, kThreads, 0, st_>>>((const bf16*)x, (bf16*)y, argmax, N, H, W, C, Ho, Wo, k, s, p);
+    launch_pool_fwd<bf16, false>(grid, st_, (const bf16*)x, nullptr, nullptr, (bf16*)y, argmax, N, H, W, C, Ho, Wo, k,
+                                 s, p);
   else
-    maxpool_fwd_kernel<float><<<grid, kThreads, 0, st_>>>((const float*)x, (float*)y, argmax, N, H, W, C, Ho, Wo, k, s,
-                                                          p);
+    launch_pool_fwd<float, false>(grid, st_, (const float*)x, nullptr, nullptr, (float*)y, argmax, N, H, W, C, Ho, Wo,
+                                  k, s, p);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
@@ -428,11 +449,10 @@ extern "C" int pose6d_bn_relu_maxpool_fwd(int32_t dtype, const void* x, const fl
   const int E = dtype == POSE6D_DT_BF16 ? 8 : 4;
   const dim3 grid(p6::ceil_div((int64_t)Wo * (C / E), kThreads), N * Ho);
   if (dtype == POSE6D_DT_BF16)
-    bn_relu_maxpool_fwd_kernel<bf16><<<grid, kThreads, 0, st_>>>((const bf16*)x, scale, shift, (bf16*)y, argmax, N, H,
-                                                                 W, C, Ho, Wo, k, s, p);
+    launch_pool_fwd<bf16, true>(grid, st_, (const bf16*)x, scale, shift, (bf16*)y, argmax, N, H, W, C, Ho, Wo, k, s, p);
   else
-    bn_relu_maxpool_fwd_kernel<float><<<grid, kThreads, 0, st_>>>((const float*)x, scale, shift, (float*)y, argmax, N,
-                                                                  H, W, C, Ho, Wo, k, s, p);
+    launch_pool_fwd<float, true>(grid, st_, (const float*)x, scale, shift, (float*)y, argmax, N, H, W, C, Ho, Wo, k, s,
+                                 p);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
@@ -445,12 +465,11 @@ extern "C" int pose6d_maxpool_bwd(int32_t dtype, const void* dy, const uint8_t* 
   if ((int64_t)N * H * W == 0) return POSE6D_OK;
   const int E = dtype == POSE6D_DT_BF16 ? 8 : 4;
   const dim3 grid(p6::ceil_div((int64_t)W * (C / E), kThreads), N * H);
+  const int nw = (k + s - 1) / s;   // windows per axis containing one input pixel, at most
   if (dtype == POSE6D_DT_BF16)
-    maxpool_bwd_kernel<bf16><<<grid, kThreads, 0, st_>>>((const bf16*)dy, argmax, (bf16*)dx, N, H, W, C, Ho, Wo, k, s,
-                                                         p);
+    launch_pool_bwd<bf16>(nw, grid, st_, (const bf16*)dy, argmax, (bf16*)dx, N, H, W, C, Ho, Wo, k, s, p);
   else
-    maxpool_bwd_kernel<float><<<grid, kThreads, 0, st_>>>((const float*)dy, argmax, (float*)dx, N, H, W, C, Ho, Wo, k,
-                                                          s, p);
+    launch_pool_bwd<float>(nw, grid, st_, (const float*)dy, argmax, (float*)dx, N, H, W, C, Ho, Wo, k, s, p);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }

@@ -340,7 +340,10 @@ def test_pools(dtype):
     from pose6d.trunk import DTYPES
     g = torch.Generator().manual_seed(4)
     dev, dt = "cuda", DTYPES[dtype]
-    for (N, H, W, C, k, s, p) in [(2, 16, 16, 64, 3, 2, 1), (2, 14, 14, 32, 2, 2, 0)]:
+    # stem 3x3/s2 and z-CNN 2x2/s2 (compile-time windows), odd extents (clamped taps),
+    # and windows that take the generic runtime-k loops (3x3/s1 backward, 5x5)
+    for (N, H, W, C, k, s, p) in [(2, 16, 16, 64, 3, 2, 1), (2, 14, 14, 32, 2, 2, 0), (1, 15, 13, 64, 3, 2, 1),
+                                  (1, 9, 9, 32, 3, 1, 1), (1, 11, 11, 32, 5, 2, 2)]:
         x = torch.randn(N, C, H, W, generator=g)
         x = F.relu(x)                         # many exact ties (zeros), as after ReLU
         if dtype == torch.bfloat16:
