@@ -8,6 +8,8 @@
 //                            backward gathers in output order (deterministic);
 //                            one lane per (pixel, 16-byte channel chunk)
 //   pose6d_avgpool_fwd/bwd   nn.AdaptiveAvgPool2d(1) + view(B, -1)
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "common.h"
@@ -15,6 +17,12 @@
 namespace {
 
 constexpr int kThreads = 256;
+
+// POSE6D_POOL_BWD_RPT (A/B only): input rows per lane of the stem pool backward
+int env_int_pool(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
 
 template <typename T> struct V;
 template <> struct V<bf16> { static constexpr int E = 8; };
@@ -311,15 +319,89 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd_kernel(const T* __restri
   st(dx + pix * C + c0, g);
 }
 
+// the compile-time-window backward for RPT consecutive input rows per lane (grid.y =
+// N * H / RPT): the candidate loads of all RPT rows are issued before the first sum,
+// so each wave keeps RPT * NW * NW window loads in flight and the grid needs RPT times
+// fewer waves (the stem pool's dx is 51 MB: one load round trip per wave, 7 rounds of
+// waves per CU at RPT = 1)
+template <typename T, int NW, int RPT>
+__global__ __launch_bounds__(kThreads) void maxpool_bwd_rows_kernel(const T* __restrict__ dy,
+                                                                    const uint8_t* __restrict__ idx,
+                                                                    T* __restrict__ dx, int N, int H, int W, int C,
+                                                                    int Ho, int Wo, int k, int s, int p) {
+  constexpr int E = V<T>::E;
+  using IdxVec = typename std::conditional<E == 8, uint2, uint32_t>::type;
+  const int cpr = C / E;
+  const int i = blockIdx.x * kThreads + threadIdx.x;  // (column, chunk) within the row
+  if (i >= W * cpr) return;
+  const int HG = H / RPT;
+  const int n = blockIdx.y / HG, iyb = (blockIdx.y - n * HG) * RPT;
+  const int ix = i / cpr, c0 = (i - ix * cpr) * E;
+  const int ox0 = max(0, (ix + p - k + s) / s), ox1 = min(Wo - 1, (ix + p) / s);
+  const int64_t nbase = (int64_t)n * Ho * Wo * C + c0;
+  uint4 draw[RPT][NW * NW];
+  IdxVec iraw[RPT][NW * NW];
+  uint8_t me[RPT][NW * NW];
+  bool ok[RPT][NW * NW];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int iy = iyb + r;
+    const int oy0 = max(0, (iy + p - k + s) / s), oy1 = min(Ho - 1, (iy + p) / s);
+#pragma unroll
+    for (int a = 0; a < NW; ++a) {
+      const int oy = oy0 + a;
+      const int cy = oy < Ho ? oy : Ho - 1;
+#pragma unroll
+      for (int b = 0; b < NW; ++b) {
+        const int ox = ox0 + b;
+        const int cx = ox < Wo ? ox : Wo - 1;
+        const int kh = iy - (oy * s - p), kw = ix - (ox * s - p);
+        const int j = a * NW + b;
+        ok[r][j] = oy <= oy1 && ox <= ox1 && kh >= 0 && kw >= 0 && kh < k && kw < k;
+        me[r][j] = (uint8_t)(kh * k + kw);
+        const int64_t o = nbase + ((int64_t)cy * Wo + cx) * C;
+        draw[r][j] = *reinterpret_cast<const uint4*>(dy + o);
+        iraw[r][j] = *reinterpret_cast<const IdxVec*>(idx + o);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    float g[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) g[e] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NW * NW; ++j) {
+      if (!ok[r][j]) continue;
+      uint8_t bi[E];
+      __builtin_memcpy(bi, &iraw[r][j], E);
+      T t[E];
+      __builtin_memcpy(t, &draw[r][j], 16);
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if (bi[e] == me[r][j]) g[e] += p6::to_f(t[e]);
+    }
+    st(dx + (((int64_t)n * H + iyb + r) * W + ix) * C + c0, g);
+  }
+}
+
 template <typename T>
 void launch_pool_bwd(int nw, dim3 grid, hipStream_t st_, const T* dy, const uint8_t* idx, T* dx, int N, int H, int W,
                      int C, int Ho, int Wo, int k, int s, int p) {
-  if (nw <= 1)
+  const int rpt = env_int_pool("POSE6D_POOL_BWD_RPT", 2);
+  if (nw == 2 && rpt == 2 && H % 2 == 0) {
+    grid.y /= 2;
+    maxpool_bwd_rows_kernel<T, 2, 2><<<grid, kThreads, 0, st_>>>(dy, idx, dx, N, H, W, C, Ho, Wo, k, s, p);
+  } else if (nw == 2 && rpt == 4 && H % 4 == 0) {
+    grid.y /= 4;
+    maxpool_bwd_rows_kernel<T, 2, 4><<<grid, kThreads, 0, st_>>>(dy, idx, dx, N, H, W, C, Ho, Wo, k, s, p);
+  } else if (nw <= 1) {
     maxpool_bwd_kernel<T, 1><<<grid, kThreads, 0, st_>>>(dy, idx, dx, N, H, W, C, Ho, Wo, k, s, p);
-  else if (nw == 2)
+  } else if (nw == 2) {
     maxpool_bwd_kernel<T, 2><<<grid, kThreads, 0, st_>>>(dy, idx, dx, N, H, W, C, Ho, Wo, k, s, p);
-  else
+  } else {
     maxpool_bwd_kernel<T, 0><<<grid, kThreads, 0, st_>>>(dy, idx, dx, N, H, W, C, Ho, Wo, k, s, p);
+  }
 }
 
 // block = 64 channel chunks (lanes) x 4 pixel groups (waves), grid (chunk groups, N);
