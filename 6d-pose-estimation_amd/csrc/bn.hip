@@ -576,32 +576,3 @@ extern "C" int pose6d_channel_sum(int32_t dtype, const void* x, int64_t M, int32
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
-
-// BN backward whose (sum dz, sum dz * xhat) partials were produced elsewhere (the
-// data-gradient epilogue of pose6d_conv2d_backward_bn): finalize + apply only.
-// partial: [2][C][rows] channel-major; workspace: 3 * C floats (coefficients).
-extern "C" int pose6d_bn_bwd_finish(int32_t dtype, const void* dout, const void* out, const float* relu_scale,
-                                    const float* relu_shift, const void* y, const float* mean, const float* invstd,
-                                    const float* gamma, float* dgamma, float* dbeta, int32_t accumulate, void* dy,
-                                    void* dz_out, const float* partial, int32_t rows, float* workspace, int64_t M,
-                                    int32_t C, void* stream) {
-  P6_CHECK_ARG(C % 8 == 0 && M > 0 && rows > 0 && partial && workspace, "pose6d_bn_bwd_finish: bad sizes");
-  P6_CHECK_ARG(!relu_scale == !relu_shift, "pose6d_bn_bwd_finish: relu_scale and relu_shift go together");
-  const int mk = out ? 1 : relu_scale ? 2 : 0;
-  hipStream_t s = p6::stream_of(stream);
-  float* coef = workspace;
-  bn_bwd_finalize_kernel<<<p6::ceil_div(C, kThreads / 64), kThreads, 0, s>>>(partial, rows, C, (double)M, gamma, invstd,
-                                                                            dgamma, dbeta, accumulate, coef);
-  P6_LAUNCH_CHECK();
-  auto apply = [&](auto* typed) {
-    using TT = std::remove_pointer_t<decltype(typed)>;
-    auto k = mk == 1 ? bn_bwd_apply_kernel<TT, 1> : mk == 2 ? bn_bwd_apply_kernel<TT, 2>
-           : mk == 3 ? bn_bwd_apply_kernel<TT, 3> : bn_bwd_apply_kernel<TT, 0>;
-    k<<<grid_for(M * C / V<TT>::E), kThreads, 0, s>>>((const TT*)dout, (const TT*)out, relu_scale, relu_shift,
-                                                      (const TT*)y, mean, invstd, coef, (TT*)dy, (TT*)dz_out, M, C);
-  };
-  if (dtype == POSE6D_DT_BF16) apply((bf16*)nullptr);
-  else apply((float*)nullptr);
-  P6_LAUNCH_CHECK();
-  return POSE6D_OK;
-}

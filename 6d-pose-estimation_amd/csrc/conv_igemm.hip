@@ -47,7 +47,6 @@ struct Geom {
   int RH, RW;              // row grid: m = (n * RH + y) * RW + x
   int KH, KW, stride, pad;
   int gm, gn;              // grid in tiles
-  int nmajor;              // fast path: tile order N-major (weights larger than the gathered source)
   int s2one;               // kDgradS2: 0 = grid covers the four parity classes; c + 1 = only class c
   // forward with the BatchNorm already known (eval): the epilogue stores
   // act(T(y) * scale + shift [+ res | + res * res_scale + res_shift]) instead of y
@@ -80,21 +79,6 @@ void s2_single_class(Geom& g, const void* res, const void* out) {
 }
 __host__ __device__ inline int s2_classes(const Geom& g) { return g.s2one ? 1 : 4; }
 
-// BatchNorm backward partials produced by a data-gradient epilogue (bf16 fast path):
-// the dX tile IS the dout of the BN that produced this conv's input, so the
-// epilogue also sums dz = dout * relu_mask and dz * xhat over its 64 rows
-// (pose6d_conv2d_backward_bn; the standalone bn_bwd reduce pass disappears).
-struct BnBwd {
-  const bf16* y;       // that BN's input (the previous conv's raw output), NHWC like dX
-  const bf16* out;     // mk 1: the forward output (mask = out > 0)
-  const float* rs;     // mk 2: mask = bf16(y * rs + rb) > 0 (ReLU recomputed)
-  const float* rb;
-  const float* mean;
-  const float* inv;
-  float* part;         // [2][C][rows] channel-major (sum dz, sum dz * xhat); null = off
-  int rows;
-  int mk;
-};
 
 // ds_read_b128 fragment reads: lanes (row = l & 15, chunk = l >> 4) of a 16-row
 // block; this XOR makes every 16-lane LDS group hit 16 distinct 16-byte slots.
@@ -129,37 +113,16 @@ __device__ __forceinline__ void load_f32s(const float* __restrict__ p, float (&f
 
 template <int NW> struct WaveGrid { static constexpr int WM = NW / 2, WN = 2, NT = 64 * NW; };
 
-template <typename T, int BM, int BN, bool BNF = false, int ACT = 0, int NW = 4, bool DUAL = false>
+template <typename T, int BM, int BN, int ACT = 0, int NW = 4, bool DUAL = false>
 __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / (16 * (NW / 2))][BN / 32], char* smem, const Geom& g,
                                               const float* __restrict__ bias, const T* __restrict__ res,
                                               T* __restrict__ out, float* __restrict__ stats, int m0, int n0,
-                                              int cls = -1, const BnBwd* bn = nullptr, int prow = 0,
-                                              const f32x4 (*acc2)[BN / 32] = nullptr) {
+                                              int cls = -1, const f32x4 (*acc2)[BN / 32] = nullptr) {
   constexpr int WM = WaveGrid<NW>::WM, NT = WaveGrid<NW>::NT;
   constexpr int TM = BM / (16 * WM), TN = BN / 32;
   static_assert(TM % 2 == 0, "BatchNorm partials cover 32-row blocks of one wave");
   constexpr int CROW = BN * (int)sizeof(T) + 16;  // epilogue tile row stride (bytes)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // BN-backward epilogue: the BN's y (and forward output) chunks this thread will
-  // need in the store loop are fetched first, so their latency overlaps the
-  // staging below instead of serialising behind each store
-  constexpr int kBnIt = (BM * (BN * (int)sizeof(T) / 16) + NT - 1) / NT;
-  uint4 pre_y[BNF ? kBnIt : 1], pre_o[BNF ? kBnIt : 1];
-  if constexpr (BNF) {
-    constexpr int CPR0 = BN * (int)sizeof(T) / 16;
-#pragma unroll
-    for (int it = 0; it < kBnIt; ++it) {
-      const int idx = tid + it * NT;
-      const int lr = idx / CPR0, cc = idx - lr * CPR0;
-      const int m = m0 + lr, c = n0 + cc * (16 / (int)sizeof(T));
-      pre_y[it] = pre_o[it] = uint4{0, 0, 0, 0};
-      if (idx < BM * CPR0 && m < g.M && c < g.Ncols) {
-        const int64_t om = out_row(g, cls, m);
-        pre_y[it] = *reinterpret_cast<const uint4*>(bn->y + om * g.Ncols + c);
-        if (bn->mk == 1) pre_o[it] = *reinterpret_cast<const uint4*>(bn->out + om * g.Ncols + c);
-      }
-    }
-  }
   constexpr int CPR = BN * (int)sizeof(T) / 16;  // 16-B chunks per tile row
   constexpr int E = 16 / (int)sizeof(T);
   constexpr int IT = (BM * CPR + NT - 1) / NT;    // store-loop trips per thread
@@ -279,18 +242,11 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / (16 * (NW / 2))]
   }
   // raw barrier: LDS writes done (lgkmcnt), the prefetched global loads stay in flight
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  constexpr bool kBnOk = BNF && sizeof(T) == 2 && CPR == 8 && NT == 256;
-  static_assert(!BNF || kBnOk, "BN-backward epilogue: bf16 64-column tiles only");
-  const bool bnf = kBnOk;
-  float bs[E], bq[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) bs[e] = bq[e] = 0.f;
   uint4 ov[IT];
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     const int idx = tid + it * NT;
     const int lr = idx < BM * CPR ? idx / CPR : 0, cc = idx - (idx / CPR) * CPR;
-    const int c = n0 + cc * E;
     uint4 v = *reinterpret_cast<const uint4*>(smem + lr * CROW + cc * 16);
     if (act) {
       // pose6d_bn_act_fwd's arithmetic on the stored (T-rounded) conv output
@@ -321,66 +277,10 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / (16 * (NW / 2))]
       __builtin_memcpy(&v, a, 16);
     }
     ov[it] = v;
-    if constexpr (kBnOk) {
-      if (bnf && okv[it]) {
-        // dout = v (as stored); dz = dout * mask; sums of dz and dz * xhat (bn_bwd_reduce2 semantics)
-        T a[E], yv[E], ovv[E];
-        __builtin_memcpy(a, &v, 16);
-        __builtin_memcpy(yv, &pre_y[it], 16);
-        __builtin_memcpy(ovv, &pre_o[it], 16);
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const float yy = p6::to_f(yv[e]);
-          bool keep = true;
-          if (bn->mk == 1) keep = p6::to_f(ovv[e]) > 0.f;
-          else if (bn->mk == 2) keep = p6::to_f(p6::from_f<T>(fmaf(yy, bn->rs[c + e], bn->rb[c + e]))) > 0.f;
-          const float d = keep ? p6::to_f(a[e]) : 0.f;
-          bs[e] += d;
-          bq[e] = fmaf(d, (yy - bn->mean[c + e]) * bn->inv[c + e], bq[e]);
-        }
-      }
-    }
   }
 #pragma unroll
   for (int it = 0; it < IT; ++it)
     if (okv[it]) *reinterpret_cast<uint4*>(out + oidx[it]) = ov[it];
-  if constexpr (kBnOk) {
-    if (bnf) {
-      // lanes with the same chunk column: tid % 8 -> fold lane bits 3..5, then 4 waves in LDS
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-#pragma unroll
-        for (int o = 8; o < 64; o <<= 1) {
-          bs[e] += __shfl_xor(bs[e], o, 64);
-          bq[e] += __shfl_xor(bq[e], o, 64);
-        }
-      }
-      __syncthreads();   // every staging read is done: reuse the tile buffer
-      float* red = reinterpret_cast<float*>(smem);   // [waves][8 chunks][2][8]
-      const int wv = tid >> 6;
-      if (lane < CPR) {
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          red[((wv * CPR + lane) * 2 + 0) * E + e] = bs[e];
-          red[((wv * CPR + lane) * 2 + 1) * E + e] = bq[e];
-        }
-      }
-      __syncthreads();
-      if (tid < BN) {
-        const int cc = tid / E, e = tid - cc * E, c = n0 + tid;
-        float s = 0.f, q = 0.f;
-#pragma unroll
-        for (int w = 0; w < kThreads / 64; ++w) {
-          s += red[((w * CPR + cc) * 2 + 0) * E + e];
-          q += red[((w * CPR + cc) * 2 + 1) * E + e];
-        }
-        if (c < g.Ncols) {
-          bn->part[(int64_t)c * bn->rows + prow] = s;
-          bn->part[((int64_t)g.Ncols + c) * bn->rows + prow] = q;
-        }
-      }
-    }
-  }
 }
 
 template <typename T, int BM, int BN, int MODE, bool ACT>
@@ -561,7 +461,7 @@ __global__ __launch_bounds__(kThreads) void conv_igemm_kernel(const T* __restric
     __syncthreads();
   }
 
-  conv_epilogue<T, BM, BN, false, ACT ? 1 : 0>(acc, smem, g, bias, res, out, stats, m0, n0);
+  conv_epilogue<T, BM, BN, ACT ? 1 : 0>(acc, smem, g, bias, res, out, stats, m0, n0);
 }
 
 // ============================================================================
@@ -657,16 +557,11 @@ template <typename T> struct LK { static constexpr int CH = 16 / (int)sizeof(T),
 
 // one workgroup's work; `bid_in` = its index in this conv's sub-grid (the whole grid,
 // or the leading part of a fused backward launch), `smem` = the kernel's dynamic LDS
-// KG = 2 (small grids): two groups of NW waves share the tile; each stage holds two
-// K-steps, group g DMAs and multiplies the g-th, and the groups' sums meet in LDS
-// before the epilogue (group 1 then leaves) -- twice the waves per SIMD on grids of
-// about one workgroup per CU, where a lone wave cannot keep the MFMA pipe busy.
-template <typename T, int BM, int BN, int MODE, int S, bool BNF = false, bool ACT = false, int NW = 4, int KG = 1>
+template <typename T, int BM, int BN, int MODE, int S, bool ACT = false, int NW = 4>
 __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* __restrict__ src,
                                               const T* __restrict__ wts, const float* __restrict__ bias,
                                               const T* __restrict__ res, T* __restrict__ out,
-                                              float* __restrict__ stats, const Geom& g,
-                                              const BnBwd* bn = nullptr) {
+                                              float* __restrict__ stats, const Geom& g) {
   constexpr int CH = LK<T>::CH, KS = LK<T>::KS;
   static_assert(KS == 64 || KS == 32, "bf16 or fp32");
   constexpr int LOG_KS = KS == 64 ? 6 : 5;
@@ -677,10 +572,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   static_assert(A_INS * RW == BM && B_INS * RW == BN, "tile rows must be a multiple of 8 x waves");
   constexpr int LOADS = A_INS + B_INS;
   constexpr int SA = BM * 128, STAGE = (BM + BN) * 128;
-  constexpr int STAGE_ALL = STAGE * KG;             // KG K-steps (slabs) per ring stage
   static_assert(S >= 2, "ring needs two stages");
-  static_assert(KG == 1 || (KG == 2 && NW == 4 && !BNF && (MODE == kGemm || MODE == kFwd)),
-                "K groups: 4-wave groups, plain forward only");
 
   const int per = g.gm * g.gn;
   const int nwg = MODE == kDgradS2 ? s2_classes(g) * per : per;
@@ -693,7 +585,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   // ids, so every XCD gets an even share of the heavy and the empty classes and the
   // four blocks that gather the same dY rows run on the same L2
   constexpr bool DUAL = MODE == kGemmDual;
-  int cls = -1, py = 0, px = 0, kh0 = 0, kw0 = 0, ntx = 1, nk = (g.Kpad >> LOG_KS) / KG;
+  int cls = -1, py = 0, px = 0, kh0 = 0, kw0 = 0, ntx = 1, nk = g.Kpad >> LOG_KS;
   const int nk1 = nk;   // kGemmDual: K-steps of the first (block) GEMM
   if (DUAL) nk += g.Kpad2 >> LOG_KS;
   if (MODE == kDgradS2) {
@@ -713,14 +605,11 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
     if (nk == 0 && res == out) return;
   }
   // consecutive logical tiles share an XCD (remap above): M-major keeps a few A row
-  // blocks + all of B in that XCD's L2, N-major all of A + a slice of B
-  int tm, tn;
-  if (g.nmajor) { tn = bid / g.gm; tm = bid - tn * g.gm; }
-  else { tm = bid / g.gn; tn = bid - tm * g.gn; }
+  // blocks + all of B in that XCD's L2
+  const int tm = bid / g.gn, tn = bid - tm * g.gn;
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane((tid >> 6) & (NW - 1));   // wave within its K group
-  const int grp = KG > 1 ? __builtin_amdgcn_readfirstlane(tid >> 6) / NW : 0;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int r8 = lane >> 3, pch = lane & 7;
   const char* zp = reinterpret_cast<const char*>(g_zero_page);
@@ -827,11 +716,10 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
 
   auto issue = [&](int kt, int buf) {
     (void)kt;
-    char* As = smem + buf * STAGE_ALL + grp * STAGE;   // group g fills slab g: K-step KG * stage + g
+    char* As = smem + buf * STAGE;
     char* Bs = As + SA;
     if (c0 == 0) set_tap();
-    const int cg = c0 + grp * KS;
-    const unsigned boff = (unsigned)(tap_koff + cg);
+    const unsigned boff = (unsigned)(tap_koff + c0);
 #pragma unroll
     for (int j = 0; j < B_INS; ++j) {
       const T* bb = b_base[j];
@@ -839,8 +727,8 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
       glds16(bb + (boff & b_mask[j]), Bs + (j * RW + wave * 8) * 128);
     }
 #pragma unroll
-    for (int i = 0; i < A_INS; ++i) glds16(a_base[i] + ((unsigned)cg & a_mask[i]), As + (i * RW + wave * 8) * 128);
-    c0 += KS * KG;
+    for (int i = 0; i < A_INS; ++i) glds16(a_base[i] + ((unsigned)c0 & a_mask[i]), As + (i * RW + wave * 8) * 128);
+    c0 += KS;
     if (c0 == tap_len) {
       c0 = 0;
       if constexpr (DUAL) {
@@ -886,7 +774,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   // mid(): issued between the fragment reads and their wait, so the next stage's
   // LDS-DMA issue (tens of cycles per instruction) overlaps the LDS read latency
   auto compute = [&](int buf, auto&& mid, auto& acc) {
-    const unsigned slot = ring_base + buf * STAGE_ALL + grp * STAGE;
+    const unsigned slot = ring_base + buf * STAGE;
     if constexpr (TM + TN == 4 && kPairedFrags) {
       unsigned addr[2][4];
 #pragma unroll
@@ -949,44 +837,18 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
     wbuf = wbuf == S - 1 ? 0 : wbuf + 1;
   }
   asm volatile("s_barrier" ::: "memory");   // every wave done reading the ring before the epilogue reuses it
-  if constexpr (KG == 2) {
-    // group 1's sums -> LDS (past the epilogue's staging area) -> added by group 0 in
-    // the same (wave, lane, tile) slots; group 1 then joins the epilogue's one barrier
-    // and leaves (no store of its own)
-    constexpr int RED = STAGE_ALL;   // offset: the second half of the 2-stage ring
-    static_assert(RED >= BM * (BN * (int)sizeof(T) + 16), "reduction area overlaps the epilogue staging");
-    f32x4* red = reinterpret_cast<f32x4*>(smem + RED);
-    if (grp == 1) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) red[((wave * TM + i) * TN + j) * 64 + lane] = acc[i][j];
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (grp == 1) {
-      asm volatile("s_barrier" ::: "memory");   // pairs with the epilogue's staging barrier
-      return;
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] += red[((wave * TM + i) * TN + j) * 64 + lane];
-  }
   if constexpr (DUAL)   // acc2 = the block GEMM, acc = the downsample branch
-    conv_epilogue<T, BM, BN, false, 1, NW, true>(acc2, smem, g, bias, nullptr, out, nullptr, m0, n0, -1, nullptr, 0,
-                                                 acc);
+    conv_epilogue<T, BM, BN, 1, NW, true>(acc2, smem, g, bias, nullptr, out, nullptr, m0, n0, -1, acc);
   else
-    conv_epilogue<T, BM, BN, BNF, ACT ? 1 : 0, NW>(acc, smem, g, bias, res, out, stats, m0, n0, cls, bn,
-                                                   MODE == kDgradS2 ? tm * 4 + cls : tm);
+    conv_epilogue<T, BM, BN, ACT ? 1 : 0, NW>(acc, smem, g, bias, res, out, stats, m0, n0, cls);
 }
 
-template <typename T, int BM, int BN, int MODE, int S, bool ACT, int NW, int KG = 1>
-__global__ __launch_bounds__(64 * NW * KG) void conv_lds_kernel(const T* __restrict__ src, const T* __restrict__ wts,
-                                                                const float* __restrict__ bias,
-                                                                const T* __restrict__ res, T* __restrict__ out,
-                                                                float* __restrict__ stats, Geom g) {
+template <typename T, int BM, int BN, int MODE, int S, bool ACT, int NW>
+__global__ __launch_bounds__(64 * NW) void conv_lds_kernel(const T* __restrict__ src, const T* __restrict__ wts,
+                                                           const float* __restrict__ bias, const T* __restrict__ res,
+                                                           T* __restrict__ out, float* __restrict__ stats, Geom g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv_lds_body<T, BM, BN, MODE, S, false, ACT, NW, KG>(smem, blockIdx.x, src, wts, bias, res, out, stats, g);
+  conv_lds_body<T, BM, BN, MODE, S, ACT, NW>(smem, blockIdx.x, src, wts, bias, res, out, stats, g);
 }
 
 // Fused backward of one conv: workgroups [0, nd) compute the data gradient,
@@ -994,17 +856,17 @@ __global__ __launch_bounds__(64 * NW * KG) void conv_lds_kernel(const T* __restr
 // each part's XCD remap intact; the padding workgroups exit at once).  Both read
 // the same dY, and the weight-gradient workgroups fill the CUs the (often small)
 // data-gradient grid leaves idle -- one launch instead of two.
-template <int DMODE, int DS, int WS, bool BNF>
+template <int DMODE, int DS, int WS>
 __global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ wt,
                                                             const bf16* __restrict__ dres, bf16* __restrict__ dx,
                                                             Geom gd, int nd, int nd_pad,
                                                             const bf16* __restrict__ x, float* __restrict__ ws,
-                                                            p6::WGeom gw, BnBwd bn, ReduceJob rj) {
+                                                            p6::WGeom gw, ReduceJob rj) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x;
   const int nw = gw.gm * gw.gn * gw.splits;
   if (b < nd_pad) {
-    if (b < nd) conv_lds_body<bf16, 64, 64, DMODE, DS, BNF>(smem, b, dy, wt, nullptr, dres, dx, nullptr, gd, &bn);
+    if (b < nd) conv_lds_body<bf16, 64, 64, DMODE, DS>(smem, b, dy, wt, nullptr, dres, dx, nullptr, gd);
   } else if (b < nd_pad + nw) {
     // kGemm data gradient <=> pointwise conv: the weight gradient takes the pointwise body
     conv_wgrad_lds_body<64, 64, WS, DMODE == kGemm>(smem, b - nd_pad, x, dy, ws, gw);
@@ -1034,15 +896,14 @@ int stage_bytes(int tile) {
   return (bm[tile] + bn[tile]) * 128;
 }
 
-template <typename T, int BM, int BN, int MODE, int S, int NW = 4, int KG = 1>
+template <typename T, int BM, int BN, int MODE, int S, int NW = 4>
 int launch_fast(const Geom& g0, const void* src, const void* w, const float* bias, const void* res, void* out,
                 float* stats, hipStream_t s) {
   Geom g = g0;
   g.gm = p6::ceil_div(g.M, BM);
   g.gn = p6::ceil_div(g.Ncols, BN);
-  const int nk = fast_nk(MODE, g, LK<T>::KS) / KG;
-  // K groups: the whole S-stage ring (the reduction area is its second stage)
-  const int ring = (KG > 1 ? S : (nk < S ? (nk > 0 ? nk : 1) : S)) * (BM + BN) * 128 * KG;
+  const int nk = fast_nk(MODE, g, LK<T>::KS);
+  const int ring = (nk < S ? (nk > 0 ? nk : 1) : S) * (BM + BN) * 128;
   // kGemmDual stages both branches' tiles for its epilogue
   const int epi = (MODE == kGemmDual ? 2 : 1) * BM * (BN * (int)sizeof(T) + 16);
   const int lds = ring > epi ? ring : epi;
@@ -1050,13 +911,13 @@ int launch_fast(const Geom& g0, const void* src, const void* w, const float* bia
   const int grid = g.gm * g.gn * (MODE == kDgradS2 ? s2_classes(g) : 1);
   if constexpr (MODE == kGemm || MODE == kFwd || MODE == kGemmDual) {
     if (g.act) {   // eval BN-act epilogue (pose6d_conv2d_fwd_act)
-      conv_lds_kernel<T, BM, BN, MODE, S, true, NW, KG><<<grid, 64 * NW * KG, lds, s>>>(
+      conv_lds_kernel<T, BM, BN, MODE, S, true, NW><<<grid, 64 * NW, lds, s>>>(
           (const T*)src, (const T*)w, bias, (const T*)res, (T*)out, stats, g);
       P6_LAUNCH_CHECK();
       return POSE6D_OK;
     }
   }
-  conv_lds_kernel<T, BM, BN, MODE, S, false, NW, KG><<<grid, 64 * NW * KG, lds, s>>>(
+  conv_lds_kernel<T, BM, BN, MODE, S, false, NW><<<grid, 64 * NW, lds, s>>>(
       (const T*)src, (const T*)w, bias, (const T*)res, (T*)out, stats, g);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
@@ -1084,10 +945,6 @@ int launch_fast_mode(const Geom& g, int tile, int stages, const void* src, const
     case 1: return launch_fast_s<T, 128, 64, MODE>(g, stages, src, w, bias, res, out, stats, s);
     case 4: return launch_fast_s<T, 128, 128, MODE, 8>(g, stages, src, w, bias, res, out, stats, s);
     case 5: return launch_fast_s<T, 128, 64, MODE, 8>(g, stages, src, w, bias, res, out, stats, s);
-    case 6:   // 64x64, two K groups of 4 waves (2 ring stages of 2 K-steps)
-      if constexpr (MODE == kGemm || MODE == kFwd) return launch_fast<T, 64, 64, MODE, 2, 4, 2>(g, src, w, bias, res,
-                                                                                               out, stats, s);
-      else return p6::set_error(POSE6D_EINVAL, "conv: K-group tile for a forward mode only");
     default: return launch_fast_s<T, 64, 64, MODE>(g, stages, src, w, bias, res, out, stats, s);
   }
 }
@@ -1179,20 +1036,18 @@ extern "C" int pose6d_conv_stats_rows(int32_t N, int32_t Ho, int32_t Wo, int32_t
   return p6::ceil_div((int64_t)N * Ho * Wo, 32);
 }
 
-int env_int(const char* name, int dflt);
-
 // implementation choice: the LDS-DMA fast path whenever each 128-byte K slice (64
 // bf16 / 32 fp32 channels) lies inside one filter tap; the register-staged kernel
-// otherwise (the Cin-4 stem, the 3- and 32-channel z-CNN layers).
-// POSE6D_CONV_F32_FAST=0 keeps fp32 on the register-staged kernel (A/B only).  POSE6D_CONV_IMPL=base|fast and POSE6D_CONV_TILE=0..3 override
-// (tuning / A-B experiments only).
+// otherwise (the Cin-4 stem, the 3- and 32-channel z-CNN layers).  A pose6d_tuning_t
+// (the *_tuned entry points: tests and tools/conv_bench.py only) can force the
+// register-staged kernel, a tile, a ring depth or the masked stride-2 gather; the
+// product entry points never take one, so each conv has one plan (one summation order).
 bool fast_ok(int dtype, int mode, const Geom& g) {
   if (mode == kFwdNarrow) return false;
   if (mode == kGemmDual) {
     const int ks2 = dtype == POSE6D_DT_BF16 ? 64 : 32;
     return g.K % ks2 == 0 && g.Kpad == g.K && g.Kpad2 % ks2 == 0;
   }
-  if (dtype == POSE6D_DT_F32 && env_int("POSE6D_CONV_F32_FAST", 1) == 0) return false;
   const int ks = dtype == POSE6D_DT_BF16 ? 64 : 32;   // elements per 128-byte K-step
   if (g.K % ks != 0 || g.Kpad != g.K) return false;
   return mode == kGemm || g.SC % ks == 0;
@@ -1213,9 +1068,9 @@ int pick_tile_fast(int dtype, int64_t M, int N, int K) {
   return (N >= 128 && K >= 256 && wg4 >= 384) ? 4 : 3;
 }
 
-int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return (v && *v) ? atoi(v) : dflt;
+// an override field of a pose6d_tuning_t, or the default (-1 / no struct)
+int tune(const pose6d_tuning_t* t, int32_t pose6d_tuning_t::*f, int dflt) {
+  return (t && t->*f >= 0) ? (int)(t->*f) : dflt;
 }
 
 struct Plan {
@@ -1231,49 +1086,25 @@ bool s2_ok(const Geom& g) {
 }
 
 // fused = the data-gradient half of conv_bwd_kernel (its workgroups are 64x64 / 4 waves)
-Plan choose(int dtype, int mode, const Geom& g, bool fused = false) {
-  const char* impl = getenv("POSE6D_CONV_IMPL");
+Plan choose(int dtype, int mode, const Geom& g, bool fused = false, const pose6d_tuning_t* tn = nullptr) {
   Plan p{};
-  p.fast = fast_ok(dtype, mode, g) && !(impl && strcmp(impl, "base") == 0);
+  p.fast = fast_ok(dtype, mode, g) && tune(tn, &pose6d_tuning_t::conv_base, 0) == 0;
   p.mode = mode;
   p.g = g;
   if (!p.fast) {
-    p.tile = env_int("POSE6D_CONV_TILE", pick_tile(g.M, g.Ncols));
+    p.tile = tune(tn, &pose6d_tuning_t::conv_tile, pick_tile(g.M, g.Ncols));
+    if (p.tile > 3) p.tile = 3;
     return p;
   }
-  if (mode == kDgrad && s2_ok(g) && env_int("POSE6D_CONV_S2", 1)) {
+  if (mode == kDgrad && s2_ok(g) && tune(tn, &pose6d_tuning_t::conv_s2, 1)) {
     p.mode = kDgradS2;
     p.g.M = g.M / 4;
     p.g.RH = g.RH / 2;
     p.g.RW = g.RW / 2;
   }
-  {
-    // POSE6D_CONV_ORDER=n: N-major tile order (A/B experiments; measured neutral on
-    // every ResNet50 layer at batch 32 -- footprints fit L2 either way)
-    const char* ord = getenv("POSE6D_CONV_ORDER");
-    p.g.nmajor = ord && ord[0] == 'n';
-  }
-  int dflt_tile = pick_tile_fast(dtype, p.g.M, g.Ncols, g.K);
-  // (never the 1x1 stride-2 downsample convs: their eval output must keep the summation
-  // order of the one-launch block kernel, pose6d_conv2d_fwd_act_dual, bit for bit)
-  if (dflt_tile == 3 && dtype == POSE6D_DT_BF16 && (p.mode == kGemm || p.mode == kFwd) &&
-      !(g.KH == 1 && g.stride == 2) && env_int("POSE6D_CONV_KG", 0)) {
-    // two K groups per 64x64 tile where a grid of ~1.5 workgroups per CU leaves the
-    // waves alone on their SIMDs: opt-in (POSE6D_CONV_KG=1).  Graph-timed single convs
-    // (profiles/r02c_conv_kgroups.txt) put layer3's 3x3 / 1x1-reduce 9-11 % and layer4's
-    // 1x1-reduce 9 % faster, but inside the eval forward graph it lost on one box,
-    // A/B alternated: 0.991 vs 0.981 ms (profiles/r02c_ab_kgroups.txt)
-    const int64_t g64 = (int64_t)p6::ceil_div(p.g.M, 64) * p6::ceil_div(g.Ncols, 64);
-    if ((g64 >= 300 && g64 <= 450) || (p.mode == kGemm && g64 <= 256 && g.K >= 2048)) dflt_tile = 6;
-  }
-  p.tile = (fused || mode == kGemmDual) ? 3 : env_int("POSE6D_CONV_TILE", dflt_tile);
-  if (p.tile == 2) p.tile = 3;   // no 64x128 instance on the fast path
-  if (p.tile == 6) {
-    // K groups: forward modes whose K-steps pair up inside every filter tap
-    const int ks = dtype == POSE6D_DT_BF16 ? 64 : 32;
-    const int tap_len = p.mode == kGemm ? g.Kpad : g.SC;
-    if (!(p.mode == kGemm || p.mode == kFwd) || tap_len % (2 * ks) != 0) p.tile = 3;
-  }
+  const int dflt_tile = pick_tile_fast(dtype, p.g.M, g.Ncols, g.K);
+  p.tile = (fused || mode == kGemmDual) ? 3 : tune(tn, &pose6d_tuning_t::conv_tile, dflt_tile);
+  if (p.tile == 2 || p.tile < 0 || p.tile > 5) p.tile = 3;   // no 64x128 instance on the fast path
   // two slots (32 KiB at 64x64) keep several workgroups per CU resident, which hides
   // the DMA latency better than a deeper ring; only long-K grids that leave CUs
   // idle (one wave of workgroups) take a 4-deep ring
@@ -1286,7 +1117,7 @@ Plan choose(int dtype, int mode, const Geom& g, bool fused = false) {
   // fp32 forward (MFMA-bound: 4 exact 16x16x4 MFMAs per 16-byte chunk): 3 slots for
   // 1x1 filters, 2 for the rest (tools/conv_bench.py --graph --dtype f32 sweep, round 2)
   if (dtype == POSE6D_DT_F32 && (p.mode == kGemm || p.mode == kFwd)) dflt = (g.KH == 1 && g.KW == 1) ? 3 : 2;
-  p.stages = env_int("POSE6D_CONV_STAGES", dflt);
+  p.stages = tune(tn, &pose6d_tuning_t::conv_stages, dflt);
   if (p.stages < 2) p.stages = 2;
   if (p.stages > 6) p.stages = 6;
   if (p.stages == 5) p.stages = 4;
@@ -1295,8 +1126,8 @@ Plan choose(int dtype, int mode, const Geom& g, bool fused = false) {
 }
 
 int run_conv(int dtype, int mode, const Geom& g, const void* src, const void* w, const float* bias, const void* res,
-             void* out, float* stats, hipStream_t s) {
-  const Plan p = choose(dtype, mode, g);
+             void* out, float* stats, hipStream_t s, const pose6d_tuning_t* tn = nullptr) {
+  const Plan p = choose(dtype, mode, g, false, tn);
   if (p.fast) return dispatch_fast(dtype, p.mode, p.g, p.tile, p.stages, src, w, bias, res, out, stats, s);
   return dtype == POSE6D_DT_BF16 ? dispatch<bf16>(mode, g, p.tile, src, w, bias, res, out, stats, s)
                                  : dispatch<float>(mode, g, p.tile, src, w, bias, res, out, stats, s);
@@ -1331,6 +1162,14 @@ Geom dgrad_geom(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stri
 extern "C" int pose6d_conv2d_fwd(int32_t dtype, const void* x, const void* w, const float* bias, void* y,
                                  float* stats, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH,
                                  int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, void* stream) {
+  return pose6d_conv2d_fwd_tuned(dtype, x, w, bias, y, stats, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo,
+                                 nullptr, stream);
+}
+
+extern "C" int pose6d_conv2d_fwd_tuned(int32_t dtype, const void* x, const void* w, const float* bias, void* y,
+                                       float* stats, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout,
+                                       int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
+                                       const pose6d_tuning_t* tuning, void* stream) {
   P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_fwd: bad dtype %d", dtype);
   P6_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cout > 0 && Cout % 8 == 0, "pose6d_conv2d_fwd: bad shape (Cout %% 8)");
   P6_CHECK_ARG(Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1,
@@ -1342,7 +1181,7 @@ extern "C" int pose6d_conv2d_fwd(int32_t dtype, const void* x, const void* w, co
     P6_CHECK_ARG(g.log2SC >= 0 && Cin % bk == 0, "pose6d_conv2d_fwd: Cin must be 4 or a power of two >= %d (got %d)",
                  bk, Cin);
   if (mode == kGemm) P6_CHECK_ARG(Cin % bk == 0, "pose6d_conv2d_fwd: 1x1 Cin %% %d != 0", bk);
-  return run_conv(dtype, mode, g, x, w, bias, nullptr, y, stats, p6::stream_of(stream));
+  return run_conv(dtype, mode, g, x, w, bias, nullptr, y, stats, p6::stream_of(stream), tuning);
 }
 
 // eval-mode conv + BatchNorm apply (+ residual, + ReLU) in one launch: the store of
@@ -1410,7 +1249,7 @@ extern "C" int pose6d_conv2d_fwd_act_dual(int32_t dtype, const void* x, const vo
 namespace {
 int dgrad_impl(int32_t dtype, const void* dy, const void* wt, const void* dres, const uint8_t* dres_mask, void* dx,
                int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
-               int32_t pad, int32_t Ho, int32_t Wo, void* stream) {
+               int32_t pad, int32_t Ho, int32_t Wo, void* stream, const pose6d_tuning_t* tn = nullptr) {
   P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_dgrad: bad dtype %d", dtype);
   P6_CHECK_ARG(stride == 1 || stride == 2, "pose6d_conv2d_dgrad: stride must be 1 or 2");
   P6_CHECK_ARG(Cin % 8 == 0, "pose6d_conv2d_dgrad: Cin %% 8 != 0 (no data gradient for the stem)");
@@ -1420,7 +1259,7 @@ int dgrad_impl(int32_t dtype, const void* dy, const void* wt, const void* dres, 
   Geom g = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
   g.res_mask = dres_mask;
   P6_CHECK_ARG(g.log2SC >= 0 && Cout % bk == 0, "pose6d_conv2d_dgrad: Cout must be a power of two >= %d", bk);
-  return run_conv(dtype, mode, g, dy, wt, nullptr, dres, dx, nullptr, p6::stream_of(stream));
+  return run_conv(dtype, mode, g, dy, wt, nullptr, dres, dx, nullptr, p6::stream_of(stream), tn);
 }
 }  // namespace
 
@@ -1430,15 +1269,23 @@ extern "C" int pose6d_conv2d_dgrad(int32_t dtype, const void* dy, const void* wt
   return dgrad_impl(dtype, dy, wt, dres, nullptr, dx, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, stream);
 }
 
+extern "C" int pose6d_conv2d_dgrad_tuned(int32_t dtype, const void* dy, const void* wt, const void* dres, void* dx,
+                                         int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH,
+                                         int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
+                                         const pose6d_tuning_t* tuning, void* stream) {
+  return dgrad_impl(dtype, dy, wt, dres, nullptr, dx, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, stream,
+                    tuning);
+}
+
 namespace {
 
 template <int DMODE, int DS, int WS>
 int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void* wt, const void* dres, void* dx,
-               const void* x, float* ws, const BnBwd& bn, const ReduceJob& rj, hipStream_t s) {
+               const void* x, float* ws, const ReduceJob& rj, hipStream_t s) {
   Geom gd = gd0;
   gd.gm = p6::ceil_div(gd.M, 64);
   gd.gn = p6::ceil_div(gd.Ncols, 64);
-  if (DMODE == kDgradS2 && !bn.part) s2_single_class(gd, dres, dx);
+  if (DMODE == kDgradS2) s2_single_class(gd, dres, dx);
   const int nd = gd.gm * gd.gn * (DMODE == kDgradS2 ? s2_classes(gd) : 1);
   const int nd_pad = (nd + 7) & ~7;
   const int nw = gw.gm * gw.gn * gw.splits;
@@ -1448,23 +1295,17 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
   const int ring_w = WS * 128 * 128;
   int lds = ring_d > epi ? ring_d : epi;
   lds = lds > ring_w ? lds : ring_w;
-  if (bn.part)
-    conv_bwd_kernel<DMODE, DS, WS, true><<<nd_pad + nw + rj.nblk, kThreads, lds, s>>>(
-        (const bf16*)dy, (const bf16*)wt, (const bf16*)dres, (bf16*)dx, gd, nd, nd_pad, (const bf16*)x, ws, gw, bn,
-        rj);
-  else
-    conv_bwd_kernel<DMODE, DS, WS, false><<<nd_pad + nw + rj.nblk, kThreads, lds, s>>>(
-        (const bf16*)dy, (const bf16*)wt, (const bf16*)dres, (bf16*)dx, gd, nd, nd_pad, (const bf16*)x, ws, gw, bn,
-        rj);
+  conv_bwd_kernel<DMODE, DS, WS><<<nd_pad + nw + rj.nblk, kThreads, lds, s>>>(
+      (const bf16*)dy, (const bf16*)wt, (const bf16*)dres, (bf16*)dx, gd, nd, nd_pad, (const bf16*)x, ws, gw, rj);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
 
 template <int DMODE>
 int launch_bwd_mode(int ds, const Geom& gd, const p6::WGeom& gw, const void* dy, const void* wt, const void* dres,
-                    void* dx, const void* x, float* ws, const BnBwd& bn, const ReduceJob& rj, hipStream_t s) {
-  return ds == 2 ? launch_bwd<DMODE, 2, 3>(gd, gw, dy, wt, dres, dx, x, ws, bn, rj, s)
-                 : launch_bwd<DMODE, 4, 3>(gd, gw, dy, wt, dres, dx, x, ws, bn, rj, s);
+                    void* dx, const void* x, float* ws, const ReduceJob& rj, hipStream_t s) {
+  return ds == 2 ? launch_bwd<DMODE, 2, 3>(gd, gw, dy, wt, dres, dx, x, ws, rj, s)
+                 : launch_bwd<DMODE, 4, 3>(gd, gw, dy, wt, dres, dx, x, ws, rj, s);
 }
 
 }  // namespace
@@ -1475,79 +1316,17 @@ int launch_bwd_mode(int ds, const Geom& gd, const p6::WGeom& gw, const void* dy,
 // otherwise as the separate pose6d_conv2d_dgrad + pose6d_conv2d_wgrad launches.
 // dx == NULL: weight gradient only.
 namespace {
-bool bwd_fused(const Plan& pd, const p6::WgradPlan& pw) {
+bool bwd_fused(const Plan& pd, const p6::WgradPlan& pw, const pose6d_tuning_t* tn) {
   return pd.fast && pd.tile == 3 && (pd.stages == 2 || pd.stages == 4) && pw.fast && pw.stages == 3 &&
-         getenv("POSE6D_BWD_SEPARATE") == nullptr;
-}
-}  // namespace
-
-extern "C" int pose6d_conv2d_backward(int32_t dtype, const void* x, const void* dy, const void* wt, const void* dres,
-                                      void* dx, float* dw, int32_t accumulate, float* workspace, int64_t ws_bytes,
-                                      int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout,
-                                      int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
-                                      void* stream) {
-  return pose6d_conv2d_backward_ex(dtype, x, dy, wt, dres, dx, dw, accumulate, workspace, ws_bytes, N, H, W, Cin,
-                                   Cin_real, Cout, KH, KW, stride, pad, Ho, Wo, 3, stream);
+         tune(tn, &pose6d_tuning_t::bwd_separate, 0) == 0;
 }
 
-namespace {
 int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void* wt, const void* dres, void* dx,
                        float* dw, int32_t accumulate, float* workspace, int64_t ws_bytes, int32_t N, int32_t H,
                        int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
-                       int32_t pad, int32_t Ho, int32_t Wo, int32_t phases, const BnBwd& bn, void* stream,
+                       int32_t pad, int32_t Ho, int32_t Wo, int32_t phases, void* stream,
                        const ReduceJob* rj = nullptr, int32_t* deferred = nullptr,
-                       const uint8_t* dres_mask = nullptr);
-}  // namespace
-
-extern "C" int pose6d_conv2d_backward_ex(int32_t dtype, const void* x, const void* dy, const void* wt,
-                                         const void* dres, void* dx, float* dw, int32_t accumulate, float* workspace,
-                                         int64_t ws_bytes, int32_t N, int32_t H, int32_t W, int32_t Cin,
-                                         int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
-                                         int32_t pad, int32_t Ho, int32_t Wo, int32_t phases, void* stream) {
-  return conv_backward_impl(dtype, x, dy, wt, dres, dx, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real,
-                            Cout, KH, KW, stride, pad, Ho, Wo, phases, BnBwd{}, stream);
-}
-
-// partial rows the fused backward's data-gradient epilogue writes for
-// pose6d_conv2d_backward_bn (one per 64-pixel tile, x4 parity classes on the
-// stride-2 path); 0 = this conv does not run the fused LDS-DMA backward
-extern "C" int pose6d_conv2d_bn_rows(int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout,
-                                     int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo) {
-  if (Cin % 8 != 0 || ilog2(Cin) < 3) return 0;
-  int mode;
-  const Geom gd0 = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
-  const Plan pd = choose(dtype, mode, gd0, true);
-  p6::WgradPlan pw;
-  p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
-  if (!bwd_fused(pd, pw)) return 0;
-  return p6::ceil_div(pd.g.M, 64) * (pd.mode == kDgradS2 ? 4 : 1);
-}
-
-extern "C" int pose6d_conv2d_backward_bn(int32_t dtype, const void* x, const void* dy, const void* wt,
-                                         const void* dres, void* dx, float* dw, int32_t accumulate, float* workspace,
-                                         int64_t ws_bytes, int32_t N, int32_t H, int32_t W, int32_t Cin,
-                                         int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
-                                         int32_t pad, int32_t Ho, int32_t Wo, const void* bn_y, const void* bn_out,
-                                         const float* bn_rs, const float* bn_rb, const float* bn_mean,
-                                         const float* bn_invstd, float* bn_part, int32_t bn_rows, int32_t bn_mk,
-                                         void* stream) {
-  const int rows = pose6d_conv2d_bn_rows(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo);
-  P6_CHECK_ARG(rows > 0 && rows == bn_rows && dx != nullptr,
-               "pose6d_conv2d_backward_bn: not on the fused path or bn_rows %d != %d", bn_rows, rows);
-  P6_CHECK_ARG(bn_y && bn_mean && bn_invstd && bn_part && bn_mk >= 0 && bn_mk <= 2 && (bn_mk != 1 || bn_out) &&
-                   (bn_mk != 2 || (bn_rs && bn_rb)),
-               "pose6d_conv2d_backward_bn: incomplete BatchNorm arguments");
-  BnBwd bn{(const bf16*)bn_y, (const bf16*)bn_out, bn_rs, bn_rb, bn_mean, bn_invstd, bn_part, bn_rows, bn_mk};
-  return conv_backward_impl(dtype, x, dy, wt, dres, dx, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real,
-                            Cout, KH, KW, stride, pad, Ho, Wo, 3, bn, stream);
-}
-
-namespace {
-int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void* wt, const void* dres, void* dx,
-                       float* dw, int32_t accumulate, float* workspace, int64_t ws_bytes, int32_t N, int32_t H,
-                       int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
-                       int32_t pad, int32_t Ho, int32_t Wo, int32_t phases, const BnBwd& bn, void* stream,
-                       const ReduceJob* rj, int32_t* deferred, const uint8_t* dres_mask) {
+                       const uint8_t* dres_mask = nullptr, const pose6d_tuning_t* tn = nullptr) {
   P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_backward: bad dtype %d", dtype);
   if (deferred) *deferred = 0;
   const ReduceJob none{};
@@ -1561,29 +1340,28 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
     if (!(phases & 1)) return POSE6D_OK;
     const int rc = flush_prev();
     if (rc) return rc;
-    return pose6d_conv2d_wgrad(dtype, x, dy, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real, Cout, KH,
-                               KW, stride, pad, Ho, Wo, stream);
+    return pose6d_conv2d_wgrad_tuned(dtype, x, dy, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real, Cout,
+                                     KH, KW, stride, pad, Ho, Wo, tn, stream);
   }
   P6_CHECK_ARG(stride == 1 || stride == 2, "pose6d_conv2d_backward: stride must be 1 or 2");
   P6_CHECK_ARG(Cin % 8 == 0 && Cin_real <= Cin && ilog2(Cin) >= 3,
                "pose6d_conv2d_backward: Cin must be a power of two >= 8 for the data gradient");
-  P6_CHECK_ARG(!dres_mask || (dres && dres != dx && !bn.part),
-               "pose6d_conv2d_backward: a residual mask needs a separate dres (and no BN epilogue)");
+  P6_CHECK_ARG(!dres_mask || (dres && dres != dx), "pose6d_conv2d_backward: a residual mask needs a separate dres");
   int mode;
   Geom gd0 = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
   gd0.res_mask = dres_mask;
-  const Plan pd = choose(dtype, mode, gd0, true);
+  const Plan pd = choose(dtype, mode, gd0, true, tn);
   p6::WgradPlan pw;
-  const p6::WGeom gw = p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
-  const bool fused = bwd_fused(pd, pw);
+  const p6::WGeom gw = p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw, tn);
+  const bool fused = bwd_fused(pd, pw, tn);
   if (!fused) {
     if (!(phases & 1)) return POSE6D_OK;
     int rc = flush_prev();
     if (rc) return rc;
-    rc = dgrad_impl(dtype, dy, wt, dres, dres_mask, dx, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, stream);
+    rc = dgrad_impl(dtype, dy, wt, dres, dres_mask, dx, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, stream, tn);
     if (rc) return rc;
-    return pose6d_conv2d_wgrad(dtype, x, dy, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real, Cout, KH,
-                               KW, stride, pad, Ho, Wo, stream);
+    return pose6d_conv2d_wgrad_tuned(dtype, x, dy, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real, Cout,
+                                     KH, KW, stride, pad, Ho, Wo, tn, stream);
   }
   P6_CHECK_ARG((int64_t)pw.splits * Cout * gw.Kpad * 4 <= ws_bytes,
                "pose6d_conv2d_backward: workspace %lld bytes < %lld needed", (long long)ws_bytes,
@@ -1594,13 +1372,13 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
   if (phases & 1) {
     switch (pd.mode) {
       case kGemm:
-        rc = launch_bwd_mode<kGemm>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, bn, carried, s);
+        rc = launch_bwd_mode<kGemm>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, carried, s);
         break;
       case kDgradS2:
-        rc = launch_bwd_mode<kDgradS2>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, bn, carried, s);
+        rc = launch_bwd_mode<kDgradS2>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, carried, s);
         break;
       default:
-        rc = launch_bwd_mode<kDgrad>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, bn, carried, s);
+        rc = launch_bwd_mode<kDgrad>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, carried, s);
         break;
     }
   }
@@ -1612,6 +1390,34 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
   return p6::wgrad_reduce_launch(workspace, dw, Cout, gw.Kpad, Cin, Cin_real, KH, KW, gw.splits, accumulate, s);
 }
 }  // namespace
+
+extern "C" int pose6d_conv2d_backward(int32_t dtype, const void* x, const void* dy, const void* wt, const void* dres,
+                                      void* dx, float* dw, int32_t accumulate, float* workspace, int64_t ws_bytes,
+                                      int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout,
+                                      int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
+                                      void* stream) {
+  return conv_backward_impl(dtype, x, dy, wt, dres, dx, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real,
+                            Cout, KH, KW, stride, pad, Ho, Wo, 3, stream);
+}
+
+extern "C" int pose6d_conv2d_backward_tuned(int32_t dtype, const void* x, const void* dy, const void* wt,
+                                            const void* dres, void* dx, float* dw, int32_t accumulate,
+                                            float* workspace, int64_t ws_bytes, int32_t N, int32_t H, int32_t W,
+                                            int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW,
+                                            int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
+                                            const pose6d_tuning_t* tuning, void* stream) {
+  return conv_backward_impl(dtype, x, dy, wt, dres, dx, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real,
+                            Cout, KH, KW, stride, pad, Ho, Wo, 3, stream, nullptr, nullptr, nullptr, tuning);
+}
+
+extern "C" int pose6d_conv2d_backward_ex(int32_t dtype, const void* x, const void* dy, const void* wt,
+                                         const void* dres, void* dx, float* dw, int32_t accumulate, float* workspace,
+                                         int64_t ws_bytes, int32_t N, int32_t H, int32_t W, int32_t Cin,
+                                         int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
+                                         int32_t pad, int32_t Ho, int32_t Wo, int32_t phases, void* stream) {
+  return conv_backward_impl(dtype, x, dy, wt, dres, dx, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real,
+                            Cout, KH, KW, stride, pad, Ho, Wo, phases, stream);
+}
 
 // launch variant of a forward / data-gradient conv, for profiling joins:
 // (stages << 12) | (fast << 8) | (mode << 4) | tile, tile 0 = 128x128, 1 = 128x64,
@@ -1636,7 +1442,7 @@ extern "C" int pose6d_bwd_variant(int32_t dtype, int32_t N, int32_t H, int32_t W
   const Plan pd = choose(dtype, mode, gd0, true);
   p6::WgradPlan pw;
   p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
-  return bwd_fused(pd, pw) ? (1 << 16) | (pd.mode << 4) | pd.stages : 0;
+  return bwd_fused(pd, pw, nullptr) ? (1 << 16) | (pd.mode << 4) | pd.stages : 0;
 }
 
 namespace {
@@ -1673,7 +1479,7 @@ extern "C" int pose6d_conv2d_backward_chain(int32_t dtype, const void* x, const 
     r = make_job(*prev);
   }
   return conv_backward_impl(dtype, x, dy, wt, dres, dx, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real,
-                            Cout, KH, KW, stride, pad, Ho, Wo, 3, BnBwd{}, stream, prev ? &r : nullptr, deferred);
+                            Cout, KH, KW, stride, pad, Ho, Wo, 3, stream, prev ? &r : nullptr, deferred);
 }
 
 extern "C" int pose6d_conv2d_backward_chain_masked(int32_t dtype, const void* x, const void* dy, const void* wt,
@@ -1691,6 +1497,5 @@ extern "C" int pose6d_conv2d_backward_chain_masked(int32_t dtype, const void* x,
     r = make_job(*prev);
   }
   return conv_backward_impl(dtype, x, dy, wt, dres, dx, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real,
-                            Cout, KH, KW, stride, pad, Ho, Wo, 3, BnBwd{}, stream, prev ? &r : nullptr, deferred,
-                            dres_mask);
+                            Cout, KH, KW, stride, pad, Ho, Wo, 3, stream, prev ? &r : nullptr, deferred, dres_mask);
 }

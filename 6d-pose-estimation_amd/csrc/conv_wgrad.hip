@@ -248,42 +248,38 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_lds_kernel(const bf16* __
   conv_wgrad_lds_body<64, 64, S, PW>(smem, blockIdx.x, x, dy, ws, g);
 }
 
-int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return (v && *v) ? atoi(v) : dflt;
+int tuned(const pose6d_tuning_t* t, int32_t pose6d_tuning_t::*f, int dflt) {
+  return (t && t->*f >= 0) ? (int)(t->*f) : dflt;
 }
 
-bool fast_ok(int dtype, int Cout, int SC) {
-  const char* impl = getenv("POSE6D_WGRAD_IMPL");
-  if (impl && strcmp(impl, "base") == 0) return false;
-  return dtype == POSE6D_DT_BF16 && SC % 64 == 0 && Cout % 64 == 0;
-}
-
-Plan plan(int dtype, int M, int Cout, int Kpad, int SC) {
+// bf16 weight gradients take the LDS-DMA kernel (64x64 tiles, 3-slot ring) unless a
+// pose6d_tuning_t (tests / tools only) asks for the register-staged kernel or another ring
+Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* tn = nullptr) {
   Plan p{};
-  p.fast = fast_ok(dtype, Cout, SC);
+  p.fast = dtype == POSE6D_DT_BF16 && SC % 64 == 0 && Cout % 64 == 0 &&
+           tuned(tn, &pose6d_tuning_t::wgrad_base, 0) == 0;
   int target, min_rows, step;
   int64_t max_bytes;
   if (p.fast) {
     p.bm = 64;
     p.bn = 64;
-    p.stages = env_int("POSE6D_WGRAD_STAGES", 3);
+    p.stages = tuned(tn, &pose6d_tuning_t::wgrad_stages, 3);
     if (p.stages < 2) p.stages = 2;
     if (p.stages > 4) p.stages = 4;
     // ~640 workgroups: fewer fp32 slabs to write and reduce than 1024, still ~2.5 per
     // CU beside the data-gradient workgroups of the fused launch (end-to-end sweep:
     // 384 / 512 / 640 / 1024 -> 5.24 / 5.16 / 5.14 / 5.20 ms per step)
-    target = env_int("POSE6D_WGRAD_BLOCKS", 640);
+    target = 640;
     min_rows = 256;
     step = 64;
     max_bytes = 48ll << 20;
   } else {
     p.bm = Cout >= 128 ? 128 : 64;
     p.bn = Kpad >= 128 ? 128 : 64;
-    target = env_int("POSE6D_WGRAD_BASE_BLOCKS", 1024);
+    target = 1024;
     min_rows = 256;
     step = MT;
-    max_bytes = (int64_t)env_int("POSE6D_WGRAD_BASE_MB", 64) << 20;   // stem: 16 -> 64 MiB of slabs, 90 -> 65 us
+    max_bytes = 64ll << 20;   // stem: 16 -> 64 MiB of slabs, 90 -> 65 us
   }
   const int tiles = p6::ceil_div(Cout, p.bm) * p6::ceil_div(Kpad, p.bn);
   // aim for ~`target` workgroups, each reducing >= min_rows pixels, slabs capped in bytes
@@ -340,25 +336,31 @@ int ilog2(int v) {
 
 }  // namespace
 
-extern "C" int64_t pose6d_conv2d_wgrad_workspace(int32_t dtype, int32_t N, int32_t Ho, int32_t Wo, int32_t Cin,
-                                                 int32_t Cout, int32_t KH, int32_t KW) {
+extern "C" int64_t pose6d_conv2d_wgrad_workspace_tuned(int32_t dtype, int32_t N, int32_t Ho, int32_t Wo, int32_t Cin,
+                                                       int32_t Cout, int32_t KH, int32_t KW,
+                                                       const pose6d_tuning_t* tuning) {
   const int bk = dtype == POSE6D_DT_BF16 ? 32 : 16;
   const int K = KH * KW * Cin;
   const int Kpad = p6::ceil_div(K, bk) * bk;
-  const Plan p = plan(dtype, N * Ho * Wo, Cout, Kpad, Cin);
+  const Plan p = plan(dtype, N * Ho * Wo, Cout, Kpad, Cin, tuning);
   return (int64_t)p.splits * Cout * Kpad * 4;
+}
+
+extern "C" int64_t pose6d_conv2d_wgrad_workspace(int32_t dtype, int32_t N, int32_t Ho, int32_t Wo, int32_t Cin,
+                                                 int32_t Cout, int32_t KH, int32_t KW) {
+  return pose6d_conv2d_wgrad_workspace_tuned(dtype, N, Ho, Wo, Cin, Cout, KH, KW, nullptr);
 }
 
 namespace p6 {
 
 WGeom wgrad_geom(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad, int Ho,
-                 int Wo, WgradPlan* plan_out) {
+                 int Wo, WgradPlan* plan_out, const pose6d_tuning_t* tuning) {
   const int bk = dtype == POSE6D_DT_BF16 ? 32 : 16;
   WGeom g{};
   g.M = N * Ho * Wo; g.Cout = Cout; g.K = KH * KW * Cin; g.Kpad = ceil_div(g.K, bk) * bk;
   g.SH = H; g.SW = W; g.SC = Cin; g.log2SC = ilog2(Cin); g.RH = Ho; g.RW = Wo;
   g.KH = KH; g.KW = KW; g.stride = stride; g.pad = pad;
-  const Plan p = plan(dtype, g.M, Cout, g.Kpad, Cin);
+  const Plan p = plan(dtype, g.M, Cout, g.Kpad, Cin, tuning);
   g.gm = ceil_div(Cout, p.bm); g.gn = ceil_div(g.Kpad, p.bn);
   g.splits = p.splits; g.mps = p.mps;
   if (plan_out) *plan_out = p;
@@ -376,14 +378,23 @@ extern "C" int pose6d_conv2d_wgrad(int32_t dtype, const void* x, const void* dy,
                                    float* workspace, int64_t ws_bytes, int32_t N, int32_t H, int32_t W, int32_t Cin,
                                    int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
                                    int32_t pad, int32_t Ho, int32_t Wo, void* stream) {
+  return pose6d_conv2d_wgrad_tuned(dtype, x, dy, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real, Cout, KH,
+                                   KW, stride, pad, Ho, Wo, nullptr, stream);
+}
+
+extern "C" int pose6d_conv2d_wgrad_tuned(int32_t dtype, const void* x, const void* dy, float* dw, int32_t accumulate,
+                                         float* workspace, int64_t ws_bytes, int32_t N, int32_t H, int32_t W,
+                                         int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW,
+                                         int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
+                                         const pose6d_tuning_t* tuning, void* stream) {
   P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_wgrad: bad dtype %d", dtype);
   P6_CHECK_ARG(ilog2(Cin) >= 2 && Cout % 8 == 0 && Cin_real <= Cin,
                "pose6d_conv2d_wgrad: Cin must be a power of two >= 4");
   Plan p;
-  const WGeom g = p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &p);
+  const WGeom g = p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &p, tuning);
   P6_CHECK_ARG((int64_t)p.splits * Cout * g.Kpad * 4 <= ws_bytes,
-               "pose6d_conv2d_wgrad: workspace %lld bytes < %lld needed (query pose6d_conv2d_wgrad_workspace with the "
-               "same environment)", (long long)ws_bytes, (long long)p.splits * Cout * g.Kpad * 4);
+               "pose6d_conv2d_wgrad: workspace %lld bytes < %lld needed (query pose6d_conv2d_wgrad_workspace[_tuned] "
+               "with the same tuning)", (long long)ws_bytes, (long long)p.splits * Cout * g.Kpad * 4);
   hipStream_t s = p6::stream_of(stream);
   int rc;
   if (p.fast) {

@@ -71,7 +71,8 @@ __global__ __launch_bounds__(kThreads) void crop_rgbd_kernel(
     const uint8_t* __restrict__ rgb, int bgr, const uint16_t* __restrict__ depth, int H, int W,
     const int32_t* __restrict__ bbox_orig, const int32_t* __restrict__ bbox_aug, const float* __restrict__ K, int S,
     const float* __restrict__ mean_std, float* __restrict__ rgb_out, float* __restrict__ depth_out,
-    float* __restrict__ depth_raw_out, float* __restrict__ center_out, float* __restrict__ K_out) {
+    float* __restrict__ depth_raw_out, float* __restrict__ center_out, float* __restrict__ K_out,
+    uint8_t* __restrict__ u8_out) {
   const int b = blockIdx.y;
   const int pix = blockIdx.x * kThreads + threadIdx.x;
   const CropGeom g = crop_geom(bbox_aug + 4 * b, H, W);
@@ -173,6 +174,10 @@ __global__ __launch_bounds__(kThreads) void crop_rgbd_kernel(
 
   // ToTensor (u8 / 255) + Normalize ((x - mean) / std), NCHW
   const int64_t plane = (int64_t)S * S;
+  if (u8_out) {   // the resized uint8 crop, HWC (the PIL image ColorJitter receives)
+    uint8_t* o = u8_out + ((int64_t)b * plane + pix) * 3;
+    o[0] = (uint8_t)outc[0]; o[1] = (uint8_t)outc[1]; o[2] = (uint8_t)outc[2];
+  }
   if (rgb_out) {
     float* o = rgb_out + (int64_t)b * 3 * plane + pix;
 #pragma unroll
@@ -207,7 +212,252 @@ extern "C" int pose6d_crop_rgbd(const uint8_t* rgb, int32_t bgr, const uint16_t*
   const dim3 grid(p6::ceil_div((int64_t)S * S, kThreads), B);
   crop_rgbd_kernel<<<grid, kThreads, 0, p6::stream_of(stream)>>>(rgb, bgr, depth, H, W, bbox_orig, bbox_aug, K, S,
                                                                  mean_std, rgb_out, depth_out, depth_raw_out,
-                                                                 center_out, K_out);
+                                                                 center_out, K_out, nullptr);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+// ---------------------------------------------------------------- train transform
+// The reference's train_transform (train_rgbd_geometric.py:41-47) on the resized
+// uint8 crop: ColorJitter(brightness, contrast, saturation, hue) in a random op order
+// -> ToTensor -> Normalize -> RandomErasing(p, scale, ratio, value 0).  ColorJitter's
+// arithmetic is Pillow's (torchvision applies it to a PIL image): ImageEnhance =
+// Image.blend against a degenerate image (black / the constant int(mean L + 0.5) /
+// the L image), float alpha, truncating; hue through Pillow's HSV conversion with
+// torchvision's uint8 hue-band shift -- restated in oracle/augment.py and pinned there
+// against Pillow itself.  One 1024-thread workgroup per crop holds the crop in LDS
+// (S * S * 3 bytes: 147 KiB at 224) while the four ops run in place, the contrast
+// mean being a workgroup reduction of the current image.
+// Random parameters: counter-based draws (splitmix64 of seed, crop, draw index) with
+// torchvision's distributions (get_params of ColorJitter / RandomErasing); every
+// crop's parameters are written to params_out so a checker can replay them.
+namespace {
+
+constexpr int kAugThreads = 1024;
+constexpr int kAugParams = 16;   // perm[4], factor[4] (NaN: op off), erase i, j, h, w (-1: none), 4 spare
+
+struct AugCfg {
+  float lo[4], hi[4];   // brightness, contrast, saturation, hue ranges (lo == hi == NaN: off)
+  float p, scale_lo, scale_hi, log_r_lo, log_r_hi;
+};
+
+__device__ __forceinline__ uint64_t splitmix(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// draw k of crop b: a uniform double in [0, 1)
+__device__ __forceinline__ double u01(uint64_t seed, int b, int k) {
+  const uint64_t x = splitmix(seed ^ splitmix(((uint64_t)(uint32_t)b << 32) | (uint32_t)k));
+  return (double)(x >> 11) * 0x1.0p-53;
+}
+
+// a float32 tensor's uniform_(lo, hi) value
+__device__ __forceinline__ float uf(uint64_t seed, int b, int k, float lo, float hi) {
+  return (float)((double)lo + ((double)hi - (double)lo) * u01(seed, b, k));
+}
+
+// Pillow ImagingBlend on one uint8 band value
+__device__ __forceinline__ int blend_u8(int d, int v, float a) {
+  if (a == 0.f) return d;
+  if (a == 1.f) return v;
+  const float t = (float)d + a * (float)(v - d);
+  if (a >= 0.f && a <= 1.f) return (int)(uint8_t)t;
+  return t <= 0.f ? 0 : (t >= 255.f ? 255 : (int)(uint8_t)t);
+}
+
+__device__ __forceinline__ int lum_u8(int r, int g, int b) { return (r * 19595 + g * 38470 + b * 7471 + 0x8000) >> 16; }
+
+__device__ __forceinline__ int clip8(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+
+// Pillow rgb2hsv_row / hsv2rgb (oracle/augment.py spells out the rounding of each step)
+__device__ __forceinline__ void rgb2hsv(int r, int g, int b, int& h8, int& s8, int& v8) {
+  const int maxc = max(r, max(g, b)), minc = min(r, min(g, b));
+  v8 = maxc;
+  if (maxc == minc) { h8 = 0; s8 = 0; return; }
+  const float cr = (float)(maxc - minc);
+  const float s = cr / (float)maxc;
+  const float rc = (float)(maxc - r) / cr, gc = (float)(maxc - g) / cr, bc = (float)(maxc - b) / cr;
+  float h;
+  if (r == maxc) h = bc - gc;
+  else if (g == maxc) h = (float)(2.0 + (double)rc - (double)bc);
+  else h = (float)(4.0 + (double)gc - (double)rc);
+  h = (float)fmod((double)h / 6.0 + 1.0, 1.0);
+  h8 = clip8((int)((double)h * 255.0));
+  s8 = clip8((int)((double)s * 255.0));
+}
+
+__device__ __forceinline__ void hsv2rgb(int h8, int s8, int v8, int& r, int& g, int& b) {
+  if (s8 == 0) { r = g = b = v8; return; }
+  const double hf = (double)(float)h8;
+  const double i = floor(hf * 6.0 / 255.0);
+  const double f = (double)(float)(hf * 6.0 / 255.0 - i);
+  const double fs = (double)(float)((double)(float)s8 / 255.0);
+  const double vf = (double)(float)v8;
+  const int p = clip8((int)round(vf * (1.0 - fs)));
+  const int q = clip8((int)round(vf * (1.0 - fs * f)));
+  const int t = clip8((int)round(vf * (1.0 - fs * (1.0 - f))));
+  switch ((int)i % 6) {
+    case 0: r = v8; g = t; b = p; break;
+    case 1: r = q; g = v8; b = p; break;
+    case 2: r = p; g = v8; b = t; break;
+    case 3: r = p; g = q; b = v8; break;
+    case 4: r = t; g = p; b = v8; break;
+    default: r = v8; g = p; b = q; break;
+  }
+}
+
+__global__ __launch_bounds__(kAugThreads) void augment_kernel(const uint8_t* __restrict__ src, int S,
+                                                              const float* __restrict__ mean_std, AugCfg cfg,
+                                                              uint64_t seed, float* __restrict__ rgb_out,
+                                                              float* __restrict__ params_out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t img[];   // [S][S][3]
+  __shared__ int red[kAugThreads / 64];
+  __shared__ float prm[kAugParams];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int npx = S * S, nbytes = npx * 3;
+  const uint8_t* in = src + (int64_t)b * nbytes;
+  for (int i = tid * 16; i < nbytes; i += kAugThreads * 16) {
+    if (i + 16 <= nbytes) {
+      *reinterpret_cast<uint4*>(img + i) = *reinterpret_cast<const uint4*>(in + i);
+    } else {
+      for (int k = i; k < nbytes; ++k) img[k] = in[k];
+    }
+  }
+  if (tid == 0) {
+    // ColorJitter.get_params: fn_idx = randperm(4), then each enabled factor
+    int perm[4] = {0, 1, 2, 3};
+    for (int i = 3; i > 0; --i) {   // Fisher-Yates
+      const int j = (int)(u01(seed, b, 3 - i) * (double)(i + 1));
+      const int t = perm[i]; perm[i] = perm[j]; perm[j] = t;
+    }
+    for (int k = 0; k < 4; ++k) {
+      prm[k] = (float)perm[k];
+      prm[4 + k] = isnan(cfg.lo[k]) ? cfg.lo[k] : uf(seed, b, 3 + k, cfg.lo[k], cfg.hi[k]);
+    }
+    // RandomErasing.forward / get_params (value 0): p, then up to 10 attempts
+    float box[4] = {-1.f, -1.f, -1.f, -1.f};
+    if (u01(seed, b, 7) < (double)cfg.p) {
+      const double area = (double)S * (double)S;
+      for (int att = 0; att < 10; ++att) {
+        const int k0 = 8 + 4 * att;
+        const double ea = area * (double)uf(seed, b, k0, cfg.scale_lo, cfg.scale_hi);
+        const double ar = (double)expf(uf(seed, b, k0 + 1, cfg.log_r_lo, cfg.log_r_hi));
+        const int h = (int)rint(sqrt(ea * ar)), w = (int)rint(sqrt(ea / ar));   // round(): half to even
+        if (!(h < S && w < S)) continue;
+        box[0] = (float)(int)(u01(seed, b, k0 + 2) * (double)(S - h + 1));
+        box[1] = (float)(int)(u01(seed, b, k0 + 3) * (double)(S - w + 1));
+        box[2] = (float)h;
+        box[3] = (float)w;
+        break;
+      }
+    }
+    for (int k = 0; k < 4; ++k) prm[8 + k] = box[k];
+    for (int k = 12; k < kAugParams; ++k) prm[k] = 0.f;
+    if (params_out)
+      for (int k = 0; k < kAugParams; ++k) params_out[b * kAugParams + k] = prm[k];
+  }
+  __syncthreads();
+  for (int step = 0; step < 4; ++step) {
+    const int op = (int)prm[step];
+    const float f = prm[4 + op];
+    if (isnan(f)) continue;   // op disabled (block-uniform)
+    int mean = 0;
+    if (op == 1) {            // contrast: int(mean(L) + 0.5) of the current image
+      int sum = 0;
+      for (int p = tid; p < npx; p += kAugThreads) sum += lum_u8(img[3 * p], img[3 * p + 1], img[3 * p + 2]);
+      sum = p6::wave_sum(sum);
+      if ((tid & 63) == 0) red[tid >> 6] = sum;
+      __syncthreads();
+      int tot = 0;
+#pragma unroll
+      for (int w = 0; w < kAugThreads / 64; ++w) tot += red[w];
+      mean = (int)((double)tot / (double)npx + 0.5);
+    }
+    const int shift = op == 3 ? ((int)(int8_t)(int)((double)f * 255.0) & 255) : 0;
+    for (int p = tid; p < npx; p += kAugThreads) {
+      int r = img[3 * p], g = img[3 * p + 1], bl = img[3 * p + 2];
+      if (op == 0) {
+        r = blend_u8(0, r, f); g = blend_u8(0, g, f); bl = blend_u8(0, bl, f);
+      } else if (op == 1) {
+        r = blend_u8(mean, r, f); g = blend_u8(mean, g, f); bl = blend_u8(mean, bl, f);
+      } else if (op == 2) {
+        const int l = lum_u8(r, g, bl);
+        r = blend_u8(l, r, f); g = blend_u8(l, g, f); bl = blend_u8(l, bl, f);
+      } else {
+        int h8, s8, v8;
+        rgb2hsv(r, g, bl, h8, s8, v8);
+        hsv2rgb((h8 + shift) & 255, s8, v8, r, g, bl);
+      }
+      img[3 * p] = (uint8_t)r; img[3 * p + 1] = (uint8_t)g; img[3 * p + 2] = (uint8_t)bl;
+    }
+    __syncthreads();
+  }
+  // ToTensor + Normalize + RandomErasing (value 0), NCHW fp32, coalesced along x
+  const int bi = (int)prm[8], bj = (int)prm[9], bh = (int)prm[10], bw = (int)prm[11];
+  float* o = rgb_out + (int64_t)b * 3 * npx;
+  for (int p = tid; p < npx; p += kAugThreads) {
+    const int y = p / S, x = p - y * S;
+    const bool erased = bh > 0 && y >= bi && y < bi + bh && x >= bj && x < bj + bw;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      float v = (float)img[3 * p + k] / 255.f;
+      if (mean_std) v = (v - mean_std[k]) / mean_std[3 + k];
+      o[(int64_t)k * npx + p] = erased ? 0.f : v;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int64_t pose6d_crop_train_workspace(int32_t B, int32_t S) { return (int64_t)B * S * S * 3; }
+
+extern "C" int pose6d_crop_rgbd_train(const uint8_t* rgb, int32_t bgr, const uint16_t* depth, int32_t B, int32_t H,
+                                      int32_t W, const int32_t* bbox_orig, const int32_t* bbox_aug, const float* K,
+                                      int32_t S, const float* mean_std, float brightness, float contrast,
+                                      float saturation, float hue, float erase_p, float erase_scale_lo,
+                                      float erase_scale_hi, float erase_ratio_lo, float erase_ratio_hi,
+                                      uint64_t seed, uint8_t* workspace, float* rgb_out, float* depth_out,
+                                      float* depth_raw_out, float* center_out, float* K_out, float* params_out,
+                                      void* stream) {
+  P6_CHECK_ARG(rgb != nullptr && bbox_aug != nullptr && workspace != nullptr && rgb_out != nullptr,
+               "pose6d_crop_rgbd_train: rgb, bbox_aug, workspace and rgb_out are required");
+  P6_CHECK_ARG(B >= 0 && H > 0 && W > 0 && S > 0 && S <= 232, "pose6d_crop_rgbd_train: bad shape (S <= 232: the "
+               "crop must fit one workgroup's LDS)");
+  P6_CHECK_ARG(center_out == nullptr || bbox_orig != nullptr, "pose6d_crop_rgbd_train: center_out needs bbox_orig");
+  P6_CHECK_ARG(K_out == nullptr || K != nullptr, "pose6d_crop_rgbd_train: K_out needs K");
+  P6_CHECK_ARG(brightness >= 0.f && contrast >= 0.f && saturation >= 0.f && hue >= 0.f && hue <= 0.5f,
+               "pose6d_crop_rgbd_train: ColorJitter factors must be >= 0 (hue <= 0.5)");
+  P6_CHECK_ARG(erase_p >= 0.f && erase_p <= 1.f && erase_scale_lo <= erase_scale_hi && erase_ratio_lo > 0.f &&
+                   erase_ratio_lo <= erase_ratio_hi,
+               "pose6d_crop_rgbd_train: bad RandomErasing arguments");
+  if (B == 0) return POSE6D_OK;
+  hipStream_t s = p6::stream_of(stream);
+  const dim3 grid(p6::ceil_div((int64_t)S * S, kThreads), B);
+  crop_rgbd_kernel<<<grid, kThreads, 0, s>>>(rgb, bgr, depth, H, W, bbox_orig, bbox_aug, K, S, nullptr, nullptr,
+                                             depth_out, depth_raw_out, center_out, K_out, workspace);
+  P6_LAUNCH_CHECK();
+  // ColorJitter._check_input: value v -> [max(0, 1 - v), 1 + v] (hue: [-v, v]); 0 -> the op is off
+  AugCfg cfg;
+  const float v[4] = {brightness, contrast, saturation, hue};
+  for (int k = 0; k < 4; ++k) {
+    if (v[k] == 0.f) {
+      cfg.lo[k] = cfg.hi[k] = __builtin_nanf("");
+    } else if (k == 3) {
+      cfg.lo[k] = -v[k]; cfg.hi[k] = v[k];
+    } else {
+      cfg.lo[k] = 1.f - v[k] > 0.f ? 1.f - v[k] : 0.f; cfg.hi[k] = 1.f + v[k];
+    }
+  }
+  cfg.p = erase_p;
+  cfg.scale_lo = erase_scale_lo;
+  cfg.scale_hi = erase_scale_hi;
+  cfg.log_r_lo = logf(erase_ratio_lo);   // torch.log(torch.tensor(ratio)): float32
+  cfg.log_r_hi = logf(erase_ratio_hi);
+  const int lds = S * S * 3;
+  augment_kernel<<<B, kAugThreads, lds, s>>>(workspace, S, mean_std, cfg, seed, rgb_out, params_out);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }

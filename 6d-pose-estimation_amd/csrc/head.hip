@@ -464,7 +464,6 @@ extern "C" int pose6d_gemm_f32_bn_eval(const float* A, int64_t sam, const float*
                                        float eps, int32_t relu, float* workspace, int64_t ws_floats, void* stream) {
   P6_CHECK_ARG(M > 0 && M <= 32 && N > 0 && K > 0, "pose6d_gemm_f32_bn_eval: batch must be 1..32 (skinny path)");
   P6_CHECK_ARG(gamma && beta && running_mean && running_var, "pose6d_gemm_f32_bn_eval: null BatchNorm1d operand");
-  P6_CHECK_ARG(getenv("POSE6D_HEAD_GENERIC") == nullptr, "pose6d_gemm_f32_bn_eval: generic GEMM forced");
   const BnEv bn{gamma, beta, running_mean, running_var, eps, relu != 0, 1};
   return gemm_f32_impl(A, sam, 1, W, 1, K, C, ldc, bias, M, N, K, 1.f, 0.f, workspace, ws_floats, bn, stream);
 }
@@ -478,7 +477,7 @@ int gemm_f32_impl(const float* A, int64_t sam, int64_t sak, const float* B, int6
   hipStream_t s = p6::stream_of(stream);
   // batch-side skinny GEMMs (nn.Linear forward / data gradient): MFMA kernel
   const bool bkc = sbk == 1, bnc = sbn == 1;
-  if (M <= 32 && sak == 1 && (bkc || bnc) && getenv("POSE6D_HEAD_GENERIC") == nullptr) {
+  if (M <= 32 && sak == 1 && (bkc || bnc)) {
     const bool vec = ((uintptr_t)A & 15) == 0 && (sam & 3) == 0 && (K & 3) == 0 &&
                      (!bkc || (((uintptr_t)B & 15) == 0 && (sbn & 3) == 0));
     // K slices: ~256 workgroups, each wave of a slice >= 16 deep (kSkW x 16 per slice),
@@ -486,7 +485,7 @@ int gemm_f32_impl(const float* A, int64_t sam, int64_t sak, const float* B, int6
     // the slices save (1024 x 512: 8.6 us in one launch)
     const int groups = p6::ceil_div(N, 16);
     int slices = 1;
-    if (workspace && groups < 256 && (int64_t)N * K >= (1 << 20) && getenv("POSE6D_SKINNY_SPLIT") == nullptr) {
+    if (workspace && groups < 256 && (int64_t)N * K >= (1 << 20)) {
       slices = p6::ceil_div(256, groups);
       const int by_k = K / (kSkW * 16);
       if (slices > by_k) slices = by_k;

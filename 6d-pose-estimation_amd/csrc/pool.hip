@@ -18,12 +18,6 @@ namespace {
 
 constexpr int kThreads = 256;
 
-// POSE6D_POOL_BWD_RPT (A/B only): input rows per lane of the stem pool backward
-int env_int_pool(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return (v && *v) ? atoi(v) : dflt;
-}
-
 template <typename T> struct V;
 template <> struct V<bf16> { static constexpr int E = 8; };
 template <> struct V<float> { static constexpr int E = 4; };
@@ -388,13 +382,10 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd_rows_kernel(const T* __r
 template <typename T>
 void launch_pool_bwd(int nw, dim3 grid, hipStream_t st_, const T* dy, const uint8_t* idx, T* dx, int N, int H, int W,
                      int C, int Ho, int Wo, int k, int s, int p) {
-  const int rpt = env_int_pool("POSE6D_POOL_BWD_RPT", 2);
-  if (nw == 2 && rpt == 2 && H % 2 == 0) {
+  // two input rows per lane (1 and 4 measured slower: profiles/r02f_pool_bwd_rows.txt)
+  if (nw == 2 && H % 2 == 0) {
     grid.y /= 2;
     maxpool_bwd_rows_kernel<T, 2, 2><<<grid, kThreads, 0, st_>>>(dy, idx, dx, N, H, W, C, Ho, Wo, k, s, p);
-  } else if (nw == 2 && rpt == 4 && H % 4 == 0) {
-    grid.y /= 4;
-    maxpool_bwd_rows_kernel<T, 2, 4><<<grid, kThreads, 0, st_>>>(dy, idx, dx, N, H, W, C, Ho, Wo, k, s, p);
   } else if (nw <= 1) {
     maxpool_bwd_kernel<T, 1><<<grid, kThreads, 0, st_>>>(dy, idx, dx, N, H, W, C, Ho, Wo, k, s, p);
   } else if (nw == 2) {

@@ -22,7 +22,7 @@ struct WgradPlan {
 
 // defined in conv_wgrad.hip
 WGeom wgrad_geom(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad, int Ho,
-                 int Wo, WgradPlan* plan);
+                 int Wo, WgradPlan* plan, const pose6d_tuning_t* tuning = nullptr);
 int wgrad_reduce_launch(const float* ws, float* dw, int Cout, int Kpad, int SC, int Cin, int KH, int KW, int splits,
                         int accumulate, hipStream_t s);
 

@@ -71,6 +71,22 @@ def load():
     return lib
 
 
+class Tuning(ctypes.Structure):
+    """pose6d_tuning_t (include/pose6d.h): explicit plan overrides for the conv
+    entry points' *_tuned forms (tests / tuning tools only; -1 = default)."""
+    _fields_ = [(n, ctypes.c_int32) for n in ("conv_tile", "conv_stages", "conv_s2", "conv_base", "wgrad_stages",
+                                               "wgrad_base", "bwd_separate")]
+
+    def __init__(self, **kw):
+        super().__init__(*([-1] * len(self._fields_)))
+        for k, v in kw.items():
+            setattr(self, k, int(v))
+
+    @property
+    def ref(self):
+        return ctypes.addressof(self)
+
+
 def symbols():
     load()
     return sorted(_lib._protos)
@@ -96,6 +112,11 @@ def call(name, *args):
     rc = fn(*conv)
     if rc != 0:
         raise Pose6dError(f"pose6d_{name} failed ({rc}): {lib.pose6d_last_error().decode()}")
+    for ob in observers:   # profiling only (pose6d.steptime maps graph nodes back to calls)
+        ob(name, args)
+
+
+observers = []
 
 
 def stream():

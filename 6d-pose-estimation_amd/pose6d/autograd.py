@@ -38,5 +38,5 @@ def run(eng, x, training, params, copy=True, **extra):
     params = [p for p in params]
     if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params)):
         return _EngineFn.apply(x, eng, training, extra, *params)
-    out = eng.forward(x, training, **extra)
+    out = eng.forward(x, training, inference=True, **extra)
     return out.clone() if copy else out

@@ -11,13 +11,17 @@ the full frames are uploaded once per batch and everything after the read --
 padding, crop, resize, ToTensor/Normalize, depth normalisation, crop-adjusted
 centre and intrinsics -- runs on the GPU.
 
-Train-mode photometric augmentation of the reference's transform (ColorJitter,
-RandomErasing on PIL images, train_*.py:41-47) is not part of this path.
+The reference's TRAIN transform (train_rgbd_geometric.py:41-47: ColorJitter(0.3,
+0.3, 0.3, 0.05) on the PIL crop, ToTensor, Normalize, RandomErasing(p=0.2,
+scale=(0.02, 0.1))) runs on the GPU too: `CropRGBD(..., augment=TrainAugment())`
+(pose6d_crop_rgbd_train -- torchvision's op order and parameter distributions,
+Pillow's uint8 arithmetic, counter-based random draws keyed by (seed, batch counter,
+crop); each crop's drawn parameters are returned for inspection / replay).
 """
 import numpy as np
 import torch
 
-from ._lib import Pose6dError, call, require_device, stream
+from ._lib import Pose6dError, call, query, require_device, stream
 
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
@@ -38,6 +42,27 @@ def jitter_bboxes(bboxes, rgbd=True, rng=np.random):
     return out
 
 
+class TrainAugment:
+    """transforms.ColorJitter(brightness, contrast, saturation, hue) +
+    transforms.RandomErasing(p, scale, ratio, value=0) of the reference's
+    train_transform (train_rgbd_geometric.py:41-47), as pose6d_crop_rgbd_train runs
+    them.  Each call of the owning CropRGBD draws fresh parameters: the kernel seed is
+    (seed, calls so far) -- deterministic for a given seed and call sequence."""
+
+    def __init__(self, brightness=0.3, contrast=0.3, saturation=0.3, hue=0.05, erase_p=0.2, erase_scale=(0.02, 0.1),
+                 erase_ratio=(0.3, 3.3), seed=0):
+        self.jitter = (float(brightness), float(contrast), float(saturation), float(hue))
+        self.erase = (float(erase_p), float(erase_scale[0]), float(erase_scale[1]), float(erase_ratio[0]),
+                      float(erase_ratio[1]))
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.calls = 0
+
+    def next_seed(self):
+        s = (self.seed * 0x9E3779B97F4A7C15 + self.calls * 0xD1B54A32D192ED03 + 1) & 0xFFFFFFFFFFFFFFFF
+        self.calls += 1
+        return s
+
+
 class CropRGBD:
     """Batched crop of full frames into the model inputs of the RGB-D datasets.
 
@@ -49,8 +74,11 @@ class CropRGBD:
     camera_matrix (B,3,3)) -- the tensors dataset_rgbd.py:206 returns, batched.
     """
 
-    def __init__(self, img_size=224, normalize=True, bgr=False, mean=IMAGENET_MEAN, std=IMAGENET_STD):
+    def __init__(self, img_size=224, normalize=True, bgr=False, mean=IMAGENET_MEAN, std=IMAGENET_STD, augment=None):
         self.img_size = img_size
+        self.augment = augment   # TrainAugment: the train transform (else the val transform)
+        self.last_params = None  # (B, 16) per-crop parameters of the last augmented call
+        self._ws = None
         self.normalize = normalize
         self.bgr = bgr
         self._ms = torch.tensor(list(mean) + list(std), dtype=torch.float32)
@@ -85,6 +113,15 @@ class CropRGBD:
         if out is None:
             out = (torch.empty(B, 3, S, S, device=dev), torch.empty(B, 1, S, S, device=dev),
                    torch.empty(B, S, S, device=dev), torch.empty(B, 2, device=dev), torch.empty(B, 3, 3, device=dev))
-        call("crop_rgbd", rgb.contiguous(), int(self.bgr), depth, B, H, W, bo, ba, Kc, S, self._mean_std(dev), *out,
-             stream())
+        if self.augment is None:
+            call("crop_rgbd", rgb.contiguous(), int(self.bgr), depth, B, H, W, bo, ba, Kc, S, self._mean_std(dev),
+                 *out, stream())
+            return out
+        nws = query("crop_train_workspace", B, S)
+        if self._ws is None or self._ws.numel() < nws or self._ws.device != dev:
+            self._ws = torch.empty(nws, device=dev, dtype=torch.uint8)
+        self.last_params = torch.empty(B, 16, device=dev)
+        a = self.augment
+        call("crop_rgbd_train", rgb.contiguous(), int(self.bgr), depth, B, H, W, bo, ba, Kc, S, self._mean_std(dev),
+             *a.jitter, *a.erase, a.next_seed(), self._ws, *out, self.last_params, stream())
         return out

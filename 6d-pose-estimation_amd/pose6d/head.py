@@ -9,8 +9,6 @@ Linear -> BatchNorm1d -> ReLU -> Dropout runs as 2 launches (GEMM + fused
 BN/ReLU/dropout column kernel), Linear -> LayerNorm -> GELU -> Dropout as 2
 (GEMM + fused row kernel); buffers are preallocated per batch size.
 """
-import os
-
 import torch
 import torch.nn as nn
 
@@ -28,6 +26,7 @@ class HeadEngine:
         self._B = None
         self.generation = 0
         self._saved_gen = -1
+        self.fuse_eval_bn = True   # False: the two separate launches (tests compare the two)
 
     @staticmethod
     def _parse(mods):
@@ -109,8 +108,10 @@ class HeadEngine:
         widest = max([in_dim] + [st.dim for st in self.stages])
         self.ws = torch.empty(16 * B * widest, device=device, dtype=torch.float32)   # split-K partials
 
-    def forward(self, x, training, seed_dev=None, salt=0):
-        """x: (B, in) fp32 device tensor -> (B, out) (engine buffer)."""
+    def forward(self, x, training, seed_dev=None, salt=0, inference=False):
+        """x: (B, in) fp32 device tensor -> (B, out) (engine buffer).  inference=True:
+        no backward will follow this forward (autograd.run's no-autograd branch), so
+        eval Linear + BatchNorm1d pairs may skip the buffers only backward reads."""
         require_device(x)
         x = x.detach().float().contiguous()
         B = x.shape[0]
@@ -120,9 +121,10 @@ class HeadEngine:
         self.x = x
         # eval without autograd: a Linear followed by an eval BatchNorm1d (no dropout)
         # stores the normalised output directly (pose6d_gemm_f32_bn_eval, bit-identical
-        # to the two launches); nothing reads the Linear's raw output then
-        fuse_bn = (not training and not torch.is_grad_enabled() and B <= 32
-                   and os.environ.get("POSE6D_HEAD_BN_FUSE", "1") != "0")
+        # to the two launches); nothing reads the Linear's raw output then.  Decided by
+        # the caller (`inference`), not by torch.is_grad_enabled(): grad mode is off
+        # inside autograd.Function.forward too, where a backward does follow
+        fuse_bn = inference and not training and B <= 32 and self.fuse_eval_bn
         skip = -1
         for i, st in enumerate(self.stages):
             st.x = cur
@@ -171,7 +173,7 @@ class HeadEngine:
             cur = st.y
         self.training = training
         self.generation += 1
-        self._saved_gen = self.generation
+        self._saved_gen = -1 if skip >= 0 else self.generation   # fused: no backward state
         return cur
 
     def backward(self, dy, grad_of, accumulate=False, need_dx=True):

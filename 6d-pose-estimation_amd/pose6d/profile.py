@@ -8,8 +8,7 @@ import torch
 from ._lib import call, query, stream
 
 # pose6d_conv_variant tile codes -> (BM, BN, waves per workgroup)
-TILES = {0: (128, 128, 4), 1: (128, 64, 4), 2: (64, 128, 4), 3: (64, 64, 4), 4: (128, 128, 8), 5: (128, 64, 8),
-         6: (64, 64, 4)}   # 6: two K groups of 4 waves, always 2 ring stages
+TILES = {0: (128, 128, 4), 1: (128, 64, 4), 2: (64, 128, 4), 3: (64, 64, 4), 4: (128, 128, 8), 5: (128, 64, 8)}
 
 
 def _tname(dtype):
@@ -20,8 +19,6 @@ def _sym(v, T):
     bm, bn, nw = TILES[v & 15]
     mode = (v >> 4) & 15
     if (v >> 8) & 1:
-        if v & 15 == 6:
-            return f"conv_lds_kernel<{T}, {bm}, {bn}, {mode}, 2, false, {nw}, 2>"
         return f"conv_lds_kernel<{T}, {bm}, {bn}, {mode}, {v >> 12}, false, {nw}>"
     return f"conv_igemm_kernel<{T}, {bm}, {bn}, {mode}, false>"
 
@@ -50,7 +47,7 @@ def conv_launches(eng, fused=True):
         if bv:
             # the step's fused data + weight gradient launch (conv2d_backward phase 1;
             # the slab reduce is its own kernel and row in rocprof)
-            sym = f"conv_bwd_kernel<{(bv >> 4) & 15}, {bv & 15}, 3, false>"
+            sym = f"conv_bwd_kernel<{(bv >> 4) & 15}, {bv & 15}, 3>"
             dw = torch.empty_like(op.conv.weight)
 
             def bwd(op=op, dw=dw):

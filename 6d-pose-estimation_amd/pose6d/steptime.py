@@ -1,0 +1,280 @@
+"""Per-kernel durations measured INSIDE a captured step (hipGraph), with HIP events.
+
+The graph of a step is captured exactly as the trainer captures it; then, before it
+is instantiated, one event-record node is spliced in front of every node and one
+after the last (hipGraphAddEventRecordNode, graph surgery through the HIP runtime
+torch already loaded).  Replaying it gives, for every kernel of the step, the time
+between the event before it and the event after it: the kernel as the step issues
+it (same arguments, same predecessor, same cache state), not an isolated replay.
+
+While the step is captured, every pose6d entry point called (pose6d._lib.call) is
+logged with the graph's node count after it, so each kernel node maps back to the
+call (and conv geometry) that launched it: that gives algorithmic flops per node.
+
+Used by bench.py for the `roofline` object and the per-symbol breakdown; rocprofv3
+--kernel-trace of the normal (uninstrumented) replay is the cross-check
+(profiles/r03*_step_trace*).
+"""
+import collections
+import ctypes
+
+import torch
+
+from . import _lib
+
+_hip = None
+
+
+def hip():
+    global _hip
+    if _hip is None:
+        h = ctypes.CDLL("libamdhip64.so.7")   # soname: the runtime torch already loaded
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        P = ctypes.POINTER
+        sig = {
+            "hipGraphGetNodes": [vp, P(vp), P(sz)],
+            "hipGraphNodeGetType": [vp, P(ctypes.c_int)],
+            "hipGraphNodeGetDependencies": [vp, P(vp), P(sz)],
+            "hipGraphRemoveDependencies": [vp, P(vp), P(vp), sz],
+            "hipGraphAddDependencies": [vp, P(vp), P(vp), sz],
+            "hipGraphAddEventRecordNode": [P(vp), vp, P(vp), sz, vp],
+            "hipGraphKernelNodeGetParams": [vp, ctypes.c_void_p],
+            "hipEventCreate": [P(vp)],
+            "hipEventDestroy": [vp],
+            "hipEventElapsedTime": [P(ctypes.c_float), vp, vp],
+            "hipStreamGetCaptureInfo_v2": [vp, P(ctypes.c_int), P(ctypes.c_ulonglong), P(vp), P(vp), P(sz)],
+        }
+        for n, a in sig.items():
+            f = getattr(h, n)
+            f.argtypes = a
+            f.restype = ctypes.c_int
+        h.hipKernelNameRefByPtr.argtypes = [vp, vp]
+        h.hipKernelNameRefByPtr.restype = ctypes.c_char_p
+        _hip = h
+    return _hip
+
+
+def _ok(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed (hipError {rc})")
+
+
+class _KernelNodeParams(ctypes.Structure):
+    _fields_ = [("block", ctypes.c_uint * 3), ("extra", ctypes.c_void_p), ("func", ctypes.c_void_p),
+                ("grid", ctypes.c_uint * 3), ("kernelParams", ctypes.c_void_p), ("sharedMemBytes", ctypes.c_uint)]
+
+
+_demangle = None
+
+
+def short_name(mangled):
+    """Demangled kernel name without namespace, return type and argument list:
+    'conv_bwd_kernel<0, 2, 3, false>' (the prefix of rocprofv3's kernel names)."""
+    global _demangle
+    if _demangle is None:
+        cxx = ctypes.CDLL("libstdc++.so.6")
+        _demangle = cxx.__cxa_demangle
+        _demangle.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+        _demangle.restype = ctypes.c_void_p
+    st = ctypes.c_int(0)
+    p = _demangle(mangled, None, None, ctypes.byref(st))
+    if st.value != 0 or not p:
+        return mangled.decode()
+    s = ctypes.string_at(p).decode()
+    ctypes.CDLL(None).free(ctypes.c_void_p(p))
+    s = s.replace("(anonymous namespace)::", "")
+    if s.startswith("void "):
+        s = s[5:]
+    depth, cut = 0, len(s)
+    for i, ch in enumerate(s):   # drop the argument list: the first '(' outside template brackets
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            cut = i
+            break
+    return s[:cut]
+
+
+def _graph_nodes(graph):
+    h = hip()
+    n = ctypes.c_size_t(0)
+    _ok(h.hipGraphGetNodes(graph, None, ctypes.byref(n)), "hipGraphGetNodes")
+    arr = (ctypes.c_void_p * max(n.value, 1))()
+    _ok(h.hipGraphGetNodes(graph, arr, ctypes.byref(n)), "hipGraphGetNodes")
+    return [arr[i] for i in range(n.value)]
+
+
+def _deps(node):
+    h = hip()
+    n = ctypes.c_size_t(0)
+    _ok(h.hipGraphNodeGetDependencies(node, None, ctypes.byref(n)), "hipGraphNodeGetDependencies")
+    arr = (ctypes.c_void_p * max(n.value, 1))()
+    _ok(h.hipGraphNodeGetDependencies(node, arr, ctypes.byref(n)), "hipGraphNodeGetDependencies")
+    return [arr[i] for i in range(n.value)]
+
+
+class _CallLog:
+    """_lib.call observer during capture: (name, args, graph node count after it)."""
+
+    def __init__(self, stream_ptr):
+        self.stream = stream_ptr
+        self.entries = []
+
+    def node_count(self):
+        h = hip()
+        status, cid = ctypes.c_int(0), ctypes.c_ulonglong(0)
+        g, deps, nd = ctypes.c_void_p(0), ctypes.c_void_p(0), ctypes.c_size_t(0)
+        _ok(h.hipStreamGetCaptureInfo_v2(ctypes.c_void_p(self.stream), ctypes.byref(status), ctypes.byref(cid),
+                                         ctypes.byref(g), ctypes.byref(deps), ctypes.byref(nd)),
+            "hipStreamGetCaptureInfo_v2")
+        if status.value != 1 or not g.value:   # 1 = hipStreamCaptureStatusActive
+            return None
+        n = ctypes.c_size_t(0)
+        _ok(hip().hipGraphGetNodes(g, None, ctypes.byref(n)), "hipGraphGetNodes")
+        return n.value
+
+    def __call__(self, name, args):
+        self.entries.append((name, args, self.node_count()))
+
+
+def conv_flops(name, args, sym):
+    """Algorithmic flops (2 per multiply-add, real input channels) of the kernel `sym`
+    launched by pose6d_<name>(*args); None for a non-conv call, 0 for the weight-
+    gradient slab reduce."""
+    if "reduce" in sym and "wgrad" in sym:
+        return 0.0
+    if name in ("conv2d_fwd", "conv2d_fwd_act"):
+        N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo = args[6:17] if name == "conv2d_fwd" else args[5:16]
+        cin = 3 if Cin == 4 else Cin   # the padded stem input (RGB padded to 4 channels)
+        return 2.0 * N * Ho * Wo * Cout * KH * KW * cin
+    if name in ("conv2d_backward_chain", "conv2d_backward_chain_masked", "conv2d_backward_bn"):
+        i0 = 11 if name == "conv2d_backward_chain_masked" else 10
+        N, H, W, Cin, Cin_real, Cout, KH, KW, stride, pad, Ho, Wo = args[i0:i0 + 12]
+        one = 2.0 * N * Ho * Wo * Cout * KH * KW * Cin_real
+        if sym.startswith("conv_bwd_kernel"):
+            return 2 * one          # data + weight gradient in one launch
+        if not args[i0 - 5]:        # dx == NULL: weight gradient only (the stem)
+            return one if "wgrad" in sym else 0.0
+        return one                  # a separate data-gradient or weight-gradient launch
+    if name == "conv2d_fwd_act_dual":
+        N, Ho, Wo, Cin, Cout, Hd, Wd, Cind = args[6:14]
+        return 2.0 * N * Ho * Wo * Cout * (Cin + Cind)
+    return None
+
+
+class StepTimer:
+    """Capture `step()` into a graph with an event before every node; `run(reps)`
+    replays it and returns one record per kernel node with its mean duration."""
+
+    def __init__(self, step, device, warm=True):
+        h = hip()
+        s = torch.cuda.Stream(device=device)
+        s.wait_stream(torch.cuda.current_stream())
+        if warm:
+            with torch.cuda.stream(s):
+                step()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph(keep_graph=True)
+        with torch.cuda.graph(self.graph, stream=s):
+            log = _CallLog(torch.cuda.current_stream().cuda_stream)
+            _lib.observers.append(log)
+            try:
+                step()
+            finally:
+                _lib.observers.remove(log)
+        raw = ctypes.c_void_p(self.graph.raw_cuda_graph())
+        nodes = _graph_nodes(raw)
+        # the capture of one stream is a chain: node i depends on node i - 1 only
+        for i, nd in enumerate(nodes):
+            d = _deps(nd)
+            if d != ([] if i == 0 else [nodes[i - 1]]):
+                raise RuntimeError("StepTimer: captured graph is not a single chain")
+        # node index -> the pose6d call that created it
+        owner = [None] * len(nodes)
+        prev = 0
+        for name, args, cnt in log.entries:
+            if cnt is None:
+                continue
+            for j in range(prev, min(cnt, len(nodes))):
+                owner[j] = (name, args)
+            prev = max(prev, cnt)
+        self.events = []
+        for i in range(len(nodes) + 1):
+            e = ctypes.c_void_p()
+            _ok(h.hipEventCreate(ctypes.byref(e)), "hipEventCreate")
+            self.events.append(e)
+        self.records = []
+        for i, nd in enumerate(nodes):
+            t = ctypes.c_int(-1)
+            _ok(h.hipGraphNodeGetType(nd, ctypes.byref(t)), "hipGraphNodeGetType")
+            sym = None
+            if t.value == 0:   # kernel node
+                p = _KernelNodeParams()
+                _ok(h.hipGraphKernelNodeGetParams(nd, ctypes.byref(p)), "hipGraphKernelNodeGetParams")
+                nm = h.hipKernelNameRefByPtr(p.func, None)
+                sym = short_name(nm) if nm else "?"
+            name, args = owner[i] if owner[i] else (None, None)
+            fl = conv_flops(name, args, sym) if (sym and name) else None
+            self.records.append({"node": i, "type": t.value, "kernel": sym, "call": name, "flops": fl})
+            # splice: deps(node) -> event_i -> node
+            ev = ctypes.c_void_p()
+            if i == 0:
+                _ok(h.hipGraphAddEventRecordNode(ctypes.byref(ev), raw, None, 0, self.events[0]), "addEventRecord")
+            else:
+                a = (ctypes.c_void_p * 1)(nodes[i - 1])
+                b = (ctypes.c_void_p * 1)(nd)
+                _ok(h.hipGraphRemoveDependencies(raw, a, b, 1), "hipGraphRemoveDependencies")
+                _ok(h.hipGraphAddEventRecordNode(ctypes.byref(ev), raw, a, 1, self.events[i]), "addEventRecord")
+            a = (ctypes.c_void_p * 1)(ev)
+            b = (ctypes.c_void_p * 1)(nd)
+            _ok(h.hipGraphAddDependencies(raw, a, b, 1), "hipGraphAddDependencies")
+        ev = ctypes.c_void_p()
+        a = (ctypes.c_void_p * 1)(nodes[-1])
+        _ok(h.hipGraphAddEventRecordNode(ctypes.byref(ev), raw, a, 1, self.events[-1]), "addEventRecord")
+        self.graph.instantiate()
+        self.stream = s
+
+    def run(self, reps=10):
+        """Replay `reps` times; each kernel record gets 'us' = mean in-step duration."""
+        h = hip()
+        n = len(self.records)
+        acc = [0.0] * n
+        total = 0.0
+        ms = ctypes.c_float(0.0)
+        for _ in range(reps + 1):
+            self.graph.replay()
+            torch.cuda.synchronize()
+            if _ == 0:
+                continue   # first replay warms the instantiated graph
+            for i in range(n):
+                _ok(h.hipEventElapsedTime(ctypes.byref(ms), self.events[i], self.events[i + 1]), "elapsed")
+                acc[i] += ms.value
+            _ok(h.hipEventElapsedTime(ctypes.byref(ms), self.events[0], self.events[n]), "elapsed")
+            total += ms.value
+        for r, a in zip(self.records, acc):
+            r["us"] = a / reps * 1e3
+        self.total_ms = total / reps
+        return [r for r in self.records if r["type"] == 0]
+
+    def close(self):
+        h = hip()
+        for e in self.events:
+            h.hipEventDestroy(e)
+        self.events = []
+
+
+def by_symbol(records):
+    """{kernel symbol: {launches, time_us, flops}} over kernel records, by total time."""
+    agg = collections.OrderedDict()
+    for r in records:
+        a = agg.setdefault(r["kernel"], {"launches": 0, "time_us": 0.0, "flops": 0.0, "flops_known": True})
+        a["launches"] += 1
+        a["time_us"] += r["us"]
+        if r["flops"] is None:
+            a["flops_known"] = False
+        else:
+            a["flops"] += r["flops"]
+    return collections.OrderedDict(sorted(agg.items(), key=lambda kv: -kv[1]["time_us"]))

@@ -146,13 +146,21 @@ class RGBDGeometricTrainer:
 
     def step_eager(self, data):
         """One training step without graphs (reference order of operations)."""
+        if self.world == 1:
+            return self.step_body(data)
         self.trunk.pack_weights(force=True)
         self._forward_loss(*data)
         dfeat = self._head_backward()
-        if self.world == 1:
-            self.trunk.backward(dfeat, self.arena.grad_of)
-        else:
-            self._backward_ddp(dfeat)
+        self._backward_ddp(dfeat)
+        self._optimizer()
+
+    def step_body(self, data):
+        """The one-GPU step's launches, in order (what capture() records for world == 1;
+        pose6d.steptime captures it for in-step kernel timing)."""
+        self.trunk.pack_weights(force=True)
+        self._forward_loss(*data)
+        dfeat = self._head_backward()
+        self.trunk.backward(dfeat, self.arena.grad_of)
         self._optimizer()
 
     # ------------------------------------------------------------- DDP backward
@@ -191,11 +199,7 @@ class RGBDGeometricTrainer:
         if self.world == 1:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self.trunk.pack_weights(force=True)
-                self._forward_loss(*data)
-                dfeat = self._head_backward()
-                self.trunk.backward(dfeat, self.arena.grad_of)
-                self._optimizer()
+                self.step_body(data)
             self.graphs = [g]
         else:
             self.graphs = self._capture_segments(data)

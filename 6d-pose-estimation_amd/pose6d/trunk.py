@@ -16,7 +16,6 @@ Only one forward's activations are kept: backward() must follow the forward it
 differentiates (checked with a generation counter).
 """
 import ctypes
-import os
 
 import numpy as np
 import torch
@@ -231,23 +230,6 @@ class TrunkEngine:
                 op.argmax = torch.empty(B, o.H, o.W, o.C, device=device, dtype=torch.uint8)
         self.ws_wgrad = f32(max(ws_w // 4, 1))
         self.ws_wgrad2 = f32(max(ws_w // 4, 1))   # ping-pong: a deferred slab reduce reads the other one
-        # BN-backward partials from the data-gradient epilogue (opt-in, POSE6D_BN_EPI=1):
-        # the conv whose input is an ActOp's output writes that BN's (sum dz, sum dz *
-        # xhat) per 64-pixel tile and the standalone reduce pass is skipped.  Measured
-        # slower at batch 32 (6.05 vs 5.70 ms/step): the epilogue work sits on the
-        # short, latency-bound data-gradient workgroups -- DESIGN.md, rejected experiments
-        producer = {id(op.out): op for op in self.ops if isinstance(op, _ActOp)}
-        fuse = os.environ.get("POSE6D_BN_EPI", "0") == "1"
-        for op in self.convs:
-            op.bn_act = producer.get(id(op.src)) if (fuse and op.needs_dgrad) else None
-            op.bn_rows = 0
-            if op.bn_act is not None:
-                op.bn_rows = query("conv2d_bn_rows", self.dt, B, op.H, op.W, op.cin_pad, op.cout, op.k, op.k,
-                                   op.stride, op.pad, op.Ho, op.Wo)
-            op.bn_part = f32(2, op.cin_pad, op.bn_rows) if op.bn_rows > 0 else None
-        for op in self.ops:
-            if isinstance(op, _ActOp):
-                op.bn_ready = None
         self.ws_bn = f32(max(ws_bn, 1))
         self.ws_fin = None   # pose6d_bn_finalize needs no workspace (one launch)
         self.feat = f32(B, self.feat_dim)
@@ -302,8 +284,11 @@ class TrunkEngine:
             self._pack_key = key
 
     # ------------------------------------------------------------ forward
-    def forward(self, x, training, pack=True):
-        """x: (B, C, H, W) fp32 on device -> features (B, feat_dim) fp32 (engine buffer)."""
+    def forward(self, x, training, pack=True, inference=False):
+        """x: (B, C, H, W) fp32 on device -> features (B, feat_dim) fp32 (engine buffer).
+        Eval mode folds each BatchNorm into its conv's epilogue: such a forward keeps no
+        backward state, so backward() after it raises (`inference` is accepted for the
+        autograd bridge; the trunk's eval forward is the same either way)."""
         require_device(x)
         B, C, H, W = x.shape
         if C != self.in_channels:
@@ -320,7 +305,7 @@ class TrunkEngine:
         call("nchw_to_nhwc", dt, xf, self.input.t, B, C, H, W, self.input.C, st)
         # eval: the BN (running statistics) is known before the conv runs, so the conv's
         # epilogue applies BN (+ residual) + ReLU and stores the activation directly
-        fold = not training and os.environ.get("POSE6D_EVAL_FUSE", "1") != "0"
+        fold = not training and self.eval_fuse
         dual = {}
         if fold:
             self._eval_fold(st)
@@ -383,6 +368,7 @@ class TrunkEngine:
         call("avgpool_fwd", dt, f.t, self.feat, B, f.H * f.W, f.C, st)
         self.generation += 1
         self._saved_gen = self.generation if training else -1
+        self._eval_gen = -1 if training else self.generation
         return self.feat
 
     def _dual_pairs(self):
@@ -393,12 +379,13 @@ class TrunkEngine:
         Only for the big-grid stages (layer1/layer2 at batch 32: >= 16384 output rows):
         the pair runs on the 64x64 tile with both accumulator sets, which lost to the
         separate launches (128x128 tiles) on layer3/layer4 (eval trace).
-        Returns {conv3: its downsample conv, downsample conv: None}; POSE6D_EVAL_DUAL=0
-        disables it, POSE6D_EVAL_DUAL_ROWS sets the row threshold."""
-        if os.environ.get("POSE6D_EVAL_DUAL", "1") == "0":
+        Returns {conv3: its downsample conv, downsample conv: None}; `eval_dual` /
+        `eval_dual_rows` (engine attributes: the tests compare both paths) switch it off /
+        set the row threshold."""
+        if not self.eval_dual:
             return {}
         ks = 64 if self.dtype == torch.bfloat16 else 32
-        min_rows = int(os.environ.get("POSE6D_EVAL_DUAL_ROWS", "16384"))
+        min_rows = self.eval_dual_rows
         pairs = {}
         for op in self.ops:
             if not isinstance(op, _ActOp) or op.res_conv is None or op.pooled:
@@ -418,6 +405,10 @@ class TrunkEngine:
         """dfeat: (B, feat_dim) fp32.  grad_of(param) -> fp32 tensor receiving that
         parameter's gradient (written, or added if accumulate).  Input gets no grad."""
         if self._saved_gen != self.generation:
+            if getattr(self, "_eval_gen", -1) == self.generation:
+                raise Pose6dError("TrunkEngine.backward after an eval-mode forward: the trunk's eval BatchNorm is "
+                                  "folded into the conv epilogues and keeps no backward state; train() the module "
+                                  "(the reference's training scripts do) to differentiate through it")
             raise Pose6dError("TrunkEngine.backward: activations of the matching training forward were overwritten")
         st = stream()
         dt = self.dt
@@ -450,14 +441,7 @@ class TrunkEngine:
                 plain = op.relu and op.res_act is None and op.res_conv is None
                 out = op.out.t if (op.relu and not plain) else None
                 rs, rb = (c.scale, c.shift) if plain else (None, None)
-                if op.bn_ready is not None:
-                    # the partial sums came with the dgrad that produced op.out.g
-                    part, rows = op.bn_ready
-                    op.bn_ready = None
-                    call("bn_bwd_finish", dt, op.out.g, out, rs, rb, c.out.t, c.mean, c.inv, bn.weight.detach(),
-                         grad_of(bn.weight), grad_of(bn.bias), acc, c.out.g, op.dz, part, rows, self.ws_bn, M,
-                         c.cout, st)
-                elif op.mbits is not None:
+                if op.mbits is not None:
                     call("bn_bwd_mask", dt, op.out.g, op.mbits, c.out.t, c.mean, c.inv, bn.weight.detach(),
                          grad_of(bn.weight), grad_of(bn.bias), acc, c.out.g, op.dz, self.ws_bn, M, c.cout, st)
                 else:
@@ -480,7 +464,6 @@ class TrunkEngine:
                 dy = op.out.g
                 M = B * op.Ho * op.Wo
                 dres, dx, dmask = None, None, None
-                final = True   # dx is the complete gradient of op.src
                 if op.needs_dgrad:
                     src = op.src
                     if src.pending is not None and src.g is not None:
@@ -495,7 +478,6 @@ class TrunkEngine:
                         # first of two contributions (conv1; the downsample conv adds to it)
                         dx = src.g
                         src.pending = src.g
-                        final = False
                     else:
                         dx = src.g
                 if op.conv.bias is not None:   # before conv_done(op) can mark the bucket ready
@@ -505,38 +487,22 @@ class TrunkEngine:
                 dw = grad_of(op.conv.weight)
                 args = (dt, op.src.t, dy, op.wt, dres, dx, dw, acc, ws, ws.numel() * 4, B, op.H, op.W, op.cin_pad,
                         op.cin, op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo)
-                a = op.bn_act
-                if a is not None and op.bn_rows > 0 and final and dx is op.src.g and dres is not dx and dmask is None:
-                    # dx is the final dout of BN `a`: its partial sums come out of this epilogue
-                    if pending is not None:
-                        call("wgrad_reduce", ctypes.addressof(pending), st)
-                        conv_done(pending_op)
-                        pending, pending_op = None, None
-                    ac = a.cop
-                    plain_a = a.relu and a.res_act is None and a.res_conv is None
-                    mk = 2 if plain_a else (1 if a.relu else 0)
-                    call("conv2d_backward_bn", *args, ac.out.t, a.out.t if mk == 1 else None,
-                         ac.scale if mk == 2 else None, ac.shift if mk == 2 else None, ac.mean, ac.inv,
-                         op.bn_part, op.bn_rows, mk, st)
-                    a.bn_ready = (op.bn_part, op.bn_rows)
-                    conv_done(op)
+                job = _WgradReduce(ws.data_ptr(), dw.data_ptr(), dt, B, op.H, op.W, op.cin_pad, op.cin, op.cout,
+                                   op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, acc)
+                prev = ctypes.addressof(pending) if pending is not None else None
+                if dmask is not None:
+                    call("conv2d_backward_chain_masked", dt, op.src.t, dy, op.wt, dres, dmask, *args[5:], prev,
+                         ctypes.addressof(deferred), st)
                 else:
-                    job = _WgradReduce(ws.data_ptr(), dw.data_ptr(), dt, B, op.H, op.W, op.cin_pad, op.cin, op.cout,
-                                       op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, acc)
-                    prev = ctypes.addressof(pending) if pending is not None else None
-                    if dmask is not None:
-                        call("conv2d_backward_chain_masked", dt, op.src.t, dy, op.wt, dres, dmask, *args[5:], prev,
-                             ctypes.addressof(deferred), st)
-                    else:
-                        call("conv2d_backward_chain", *args, prev, ctypes.addressof(deferred), st)
-                    if pending_op is not None:
-                        conv_done(pending_op)          # its reduce ran in this launch (or just before it)
-                    if deferred.value:
-                        pending, pending_op = job, op
-                        slot ^= 1
-                    else:
-                        pending, pending_op = None, None
-                        conv_done(op)
+                    call("conv2d_backward_chain", *args, prev, ctypes.addressof(deferred), st)
+                if pending_op is not None:
+                    conv_done(pending_op)          # its reduce ran in this launch (or just before it)
+                if deferred.value:
+                    pending, pending_op = job, op
+                    slot ^= 1
+                else:
+                    pending, pending_op = None, None
+                    conv_done(op)
 
             else:
                 s = op.src
@@ -557,6 +523,13 @@ class TrunkEngine:
         return False
 
     dtype_req = torch.float32
+    # eval-forward fusions (bit-identical to the separate launches; attributes, not
+    # environment, so the tests can compare both paths): BN + residual + ReLU in the conv
+    # epilogue, and a downsampling block's two convs in one launch for >= eval_dual_rows
+    # output rows
+    eval_fuse = True
+    eval_dual = True
+    eval_dual_rows = 16384
 
     def set_dtype(self, dtype):
         self.dtype_req = dtype

@@ -171,9 +171,7 @@ def main():
     ap.add_argument("--no-kernel-profile", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
     ap.add_argument("--no-side", action="store_true", help="skip the configs[1] / configs[3] side measurements")
-    ap.add_argument("--roofline-only", action="store_true",
-                    help="one eager step + the per-kernel roofline replays only (the command whose rocprofv3 "
-                         "--stats summary profiles/*_roofline_stats.csv holds: same launches, same averages)")
+    ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 (reference precision) training line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -200,11 +198,6 @@ def main():
     B = args.batch
     tr = RGBDGeometricTrainer(model, B, dtype=torch.bfloat16, process_group=pg)
     data = synth_batch(B, dev, seed=1000 + rank)   # each rank its own shard
-    if args.roofline_only:
-        tr.step_eager(data)
-        torch.cuda.synchronize()
-        print(json.dumps(kernel_profile(tr, float("nan"), with_forward=False)), flush=True)
-        return
     if not args.eager:
         tr.capture(data)
     for _ in range(args.warmup):
@@ -233,14 +226,22 @@ def main():
         "metric": "crops/sec training RGBD-Geometric bs32 224^2 (per GPU), fwd+geodesic/L1 loss+bwd+clip+AdamW",
         "value": round(value, 2), "unit": "crops/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "bf16", "data": "synthetic (SURVEY.md §8d shapes, device-resident)",
+        "vs_baseline": None, "dtype": "bf16",
+        "dtype_note": "bf16 trunk activations / MFMA operands as BASELINE configs[2] names (fp32 accumulation, "
+                      "BN statistics, heads, loss, AdamW): narrower than the reference's fp32 training; the "
+                      "reference-precision step is the fp32_train line",
+        "data": "synthetic (SURVEY.md §8d shapes, device-resident)",
         "config": {"workload": "PoseNetRGBDGeometric train step (BASELINE configs[2]; configs[4] at N>1)",
                    "model": "PoseNetRGBDGeometric (ResNet50 + BN-MLP rot head, pinhole translation)",
                    "global_batch": world * B, "per_gpu_batch": B, "crop": "224x224", "seq_len": None,
                    "parallelism": f"dp{world}", "loss": float(loss)},
     }
     if rank == 0 and not args.no_kernel_profile:
-        result.update(kernel_profile(tr, ms))
+        result.update(kernel_profile(tr, data, ms))
+    if rank == 0 and not args.no_fp32:
+        # the same step in the reference's fp32 arithmetic (this headline line is bf16,
+        # BASELINE configs[2]: narrower than the reference's fp32 training)
+        result["fp32_train"] = fp32_train(dev, args.steps, args.warmup, B)
     if rank == 0 and not args.no_side:
         result["side_configs"] = {"configs[1]": rgb_fp32_forward(dev), "dropin_fp32_train": dropin_fp32_train(dev),
                                   "configs[3]": add_eval_throughput(dev, cpu=not args.no_cpu_baseline),
@@ -262,48 +263,95 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def kernel_profile(tr, step_ms, with_forward=True):
-    """Dominant kernel (largest total time per step) -> roofline object, plus the
-    forward-pass HBM roofline fraction (the north-star's 60 % target)."""
-    from pose6d import profile
-    timed = profile.time_launches(profile.conv_launches(tr.trunk), reps=10)
-    agg = profile.by_symbol(timed)
-    sym, a = max(agg.items(), key=lambda kv: kv[1]["time_s"])
-    avg_t = a["time_s"] / a["launches"]
+def kernel_profile(tr, data, step_ms, peak_tflops=None, with_forward=True, reps=10):
+    """Dominant kernel of the step (largest total in-step time among the conv
+    kernels, whose algorithmic flops are known) -> roofline object, timed INSIDE the
+    captured step (pose6d.steptime: an event node spliced before every kernel node of
+    the step's graph -- same launches, arguments and cache state as the timed step),
+    plus the per-symbol in-step breakdown and the forward-pass HBM roofline
+    fractions (the north-star's 60 % target)."""
+    from pose6d import steptime
+    if peak_tflops is None:
+        peak_tflops = PEAK_BF16_TFLOPS if tr.trunk.dtype == torch.bfloat16 else PEAK_F32_MFMA_TFLOPS
+    timer = steptime.StepTimer(lambda: tr.step_body(data), tr.dev)
+    recs = timer.run(reps)
+    inst_ms = timer.total_ms
+    timer.close()
+    agg = steptime.by_symbol(recs)
+    conv = {k: v for k, v in agg.items() if v["flops_known"] and v["flops"] > 0}
+    sym, a = max(conv.items(), key=lambda kv: kv[1]["time_us"])
+    avg_t = a["time_us"] / a["launches"] * 1e-6
     achieved = a["flops"] / a["launches"] / avg_t / 1e12
-    conv_total_ms = sum(v["time_s"] for v in agg.values()) * 1e3
-    # forward-only (training-mode BN) time of the trunk, graph-captured
-    fwd_ms = forward_time(tr) if with_forward else float("nan")
-    fwd_gbs = FWD_BYTES_PER_CROP * tr.B / (fwd_ms * 1e-3) / 1e9
-    # eval-mode forward of the whole model (BN folded into the conv epilogues), graph-captured
-    ev_ms = eval_forward_time(tr.dev, tr.B) if with_forward else float("nan")
-    ev_gbs = FWD_BYTES_PER_CROP * tr.B / (ev_ms * 1e-3) / 1e9
+    conv_total_ms = sum(v["time_us"] for v in conv.values()) * 1e-3
+    busy_ms = sum(r["us"] for r in recs) * 1e-3
     pmc, tsrc = pmc_traffic(sym)
     traffic = round(pmc["hbm_bytes_per_launch"]) if pmc else None
-    # SQ_VALU_MFMA_BUSY_CYCLES = 16 cycles per 16x16x32 MFMA summed over the chip's
-    # 1024 SIMDs; busy fraction at the 2.4 GHz clock
+    # SQ_VALU_MFMA_BUSY_CYCLES summed over the chip's 1024 SIMDs; busy fraction at 2.4 GHz
     mfma_busy = (round(pmc["mfma_busy_cycles_per_launch"] / (avg_t * 2.4e9 * 1024), 4)
                  if pmc and "mfma_busy_cycles_per_launch" in pmc else None)
-    return {
-        "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+    out = {
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak_tflops, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak_tflops, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
                      "traffic_source": tsrc, "mfma_busy": mfma_busy,
                      "kernel": sym, "launches_per_step": a["launches"],
                      "avg_launch_us": round(avg_t * 1e6, 2),
-                     "algorithmic_flops_per_launch": a["flops"] / a["launches"]},
-        "breakdown": {"conv_kernels_ms_per_step": round(conv_total_ms, 3), "step_ms": round(step_ms, 3),
-                      "by_symbol_ms": {k: round(v["time_s"] * 1e3, 3) for k, v in agg.items()}},
-        "forward_roofline": {"bound": "hbm", "fwd_ms": round(fwd_ms, 4), "achieved": round(fwd_gbs, 1),
-                             "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(fwd_gbs / PEAK_HBM_GBS, 4),
-                             "algorithmic_bytes_per_crop": FWD_BYTES_PER_CROP,
-                             "mode": "trunk forward inside the training step (batch statistics)"},
-        "forward_roofline_eval": {"bound": "hbm", "fwd_ms": round(ev_ms, 4), "achieved": round(ev_gbs, 1),
-                                  "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ev_gbs / PEAK_HBM_GBS, 4),
-                                  "algorithmic_bytes_per_crop": FWD_BYTES_PER_CROP,
-                                  "crops_per_s": round(tr.B / (ev_ms * 1e-3), 1),
-                                  "mode": "PoseNetRGBDGeometric eval forward bs32 bf16 (running-stat BN folded into "
-                                          "the conv epilogues), hipGraph replay"},
+                     "algorithmic_flops_per_launch": a["flops"] / a["launches"],
+                     "timing": "in-step: HIP event nodes spliced around every kernel node of the captured step "
+                               f"graph (pose6d/steptime.py), mean over {reps} replays"},
+        "breakdown": {"kernels_per_step": len(recs), "gpu_busy_ms_per_step": round(busy_ms, 3),
+                      "instrumented_step_ms": round(inst_ms, 3), "step_ms": round(step_ms, 3),
+                      "conv_kernels_ms_per_step": round(conv_total_ms, 3),
+                      "by_symbol": {k: {"launches": v["launches"], "ms": round(v["time_us"] * 1e-3, 4),
+                                        "avg_us": round(v["time_us"] / v["launches"], 2),
+                                        **({"tflops": round(v["flops"] / (v["time_us"] * 1e-6) / 1e12, 1)}
+                                           if v["flops_known"] and v["flops"] > 0 else {})}
+                                    for k, v in agg.items()}},
     }
+    if with_forward:
+        # forward-only (training-mode BN) time of the trunk, graph-captured
+        fwd_ms = forward_time(tr)
+        fwd_gbs = FWD_BYTES_PER_CROP * tr.B / (fwd_ms * 1e-3) / 1e9
+        # eval-mode forward of the whole model (BN folded into the conv epilogues), graph-captured
+        ev_ms = eval_forward_time(tr.dev, tr.B)
+        ev_gbs = FWD_BYTES_PER_CROP * tr.B / (ev_ms * 1e-3) / 1e9
+        out["forward_roofline"] = {"bound": "hbm", "fwd_ms": round(fwd_ms, 4), "achieved": round(fwd_gbs, 1),
+                                   "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(fwd_gbs / PEAK_HBM_GBS, 4),
+                                   "algorithmic_bytes_per_crop": FWD_BYTES_PER_CROP,
+                                   "mode": "trunk forward inside the training step (batch statistics)"}
+        out["forward_roofline_eval"] = {"bound": "hbm", "fwd_ms": round(ev_ms, 4), "achieved": round(ev_gbs, 1),
+                                        "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ev_gbs / PEAK_HBM_GBS, 4),
+                                        "algorithmic_bytes_per_crop": FWD_BYTES_PER_CROP,
+                                        "crops_per_s": round(tr.B / (ev_ms * 1e-3), 1),
+                                        "mode": "PoseNetRGBDGeometric eval forward bs32 bf16 (running-stat BN folded "
+                                                "into the conv epilogues), hipGraph replay"}
+    return out
+
+
+def fp32_train(dev, steps, warmup, B=32):
+    """The reference's own arithmetic (train_rgbd_geometric.py:106-112 trains in fp32,
+    SURVEY.md §2.2): the fused RGBDGeometricTrainer step with fp32 activations and
+    MFMA operands (exact v_mfma_f32_16x16x4_f32), graph-replayed at bs32, with its own
+    in-step roofline against the fp32 MFMA peak."""
+    from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
+    from pose6d.train import RGBDGeometricTrainer
+    torch.manual_seed(0)
+    model = PoseNetRGBDGeometric(pretrained=False).to(dev)
+    tr = RGBDGeometricTrainer(model, B, dtype=torch.float32)
+    data = synth_batch(B, dev, seed=1000)
+    tr.capture(data)
+    for _ in range(warmup):
+        tr.step(data)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.step(data)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    kp = kernel_profile(tr, data, ms, PEAK_F32_MFMA_TFLOPS, with_forward=False)
+    return {"workload": "PoseNetRGBDGeometric train step, bs32 224^2, fp32 end to end (the reference's precision), "
+                        "fused RGBDGeometricTrainer, hipGraph replay",
+            "value": round(B / (ms * 1e-3), 2), "unit": "crops/s", "ms_per_step": round(ms, 4), "steps": steps,
+            "dtype": "f32", "loss": float(tr.loss.item()), **kp}
 
 
 def pmc_traffic(sym):
@@ -456,6 +504,11 @@ def crop_throughput(dev, B=32, reps=20):
     crop = CropRGBD(S)
     out = crop(*args)
     t = _time_fn(lambda: crop(*args, out=out), reps)
+    # the train transform (train_rgbd_geometric.py:41-47): + ColorJitter + RandomErasing
+    from pose6d.data import TrainAugment
+    crop_tr = CropRGBD(S, augment=TrainAugment(seed=0))
+    crop_tr(*args, out=out)
+    t_tr = _time_fn(lambda: crop_tr(*args, out=out), reps)
     nbytes = 0
     for x, y, ww, hh in ba.tolist():
         size = max(ww, hh) * 1.2
@@ -466,6 +519,9 @@ def crop_throughput(dev, B=32, reps=20):
     gbs = nbytes / t / 1e9
     return {"workload": f"pose6d_crop_rgbd: {B} frames 640x480 -> 224^2 model inputs (val transform)",
             "value": round(B / t, 1), "unit": "crops/s", "ms_per_batch": round(t * 1e3, 4), "dtype": "u8/u16->f32",
+            "train_transform": {"workload": "pose6d_crop_rgbd_train: the same crops + ColorJitter(0.3, 0.3, 0.3, "
+                                            "0.05) + RandomErasing(0.2, (0.02, 0.1)) (train_rgbd_geometric.py:41-47)",
+                                "value": round(B / t_tr, 1), "unit": "crops/s", "ms_per_batch": round(t_tr * 1e3, 4)},
             "hbm_roofline": {"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": round(gbs / PEAK_HBM_GBS, 4), "algorithmic_bytes_per_batch": round(nbytes)}}
 

@@ -137,6 +137,27 @@ int pose6d_crop_rgbd(const uint8_t *rgb, int32_t bgr, const uint16_t *depth, int
                      const float *mean_std, float *rgb_out, float *depth_out, float *depth_raw_out,
                      float *center_out, float *K_out, void *stream);
 
+/* ----------------------------------------------------------------------
+ * Train transform of the same crops (train_rgbd_geometric.py:41-47, applied by
+ * dataset_rgbd.py:196-197): pose6d_crop_rgbd's crop + resize, then on the uint8
+ * crop ColorJitter(brightness, contrast, saturation, hue) with torchvision's op
+ * order / factor draws and Pillow's arithmetic, ToTensor + Normalize, then
+ * RandomErasing(erase_p, (erase_scale_lo, _hi), (erase_ratio_lo, _hi), value 0).
+ * A jitter value of 0 switches that op off (torchvision's None).  Random draws:
+ * counter-based (seed, crop, draw) -- the same seed gives the same crops; each crop's
+ * drawn parameters go to params_out [B][16] (may be NULL): perm[4], brightness,
+ * contrast, saturation, hue factor (NaN = off), erase i, j, h, w (-1 = none), 0 x 4.
+ * workspace: pose6d_crop_train_workspace(B, S) bytes (the uint8 crops).  S <= 232.
+ * rgb_out is required; the depth / centre / K outputs as pose6d_crop_rgbd.
+ * ---------------------------------------------------------------------- */
+int64_t pose6d_crop_train_workspace(int32_t B, int32_t S);
+int pose6d_crop_rgbd_train(const uint8_t *rgb, int32_t bgr, const uint16_t *depth, int32_t B, int32_t H, int32_t W,
+                           const int32_t *bbox_orig, const int32_t *bbox_aug, const float *K, int32_t S,
+                           const float *mean_std, float brightness, float contrast, float saturation, float hue,
+                           float erase_p, float erase_scale_lo, float erase_scale_hi, float erase_ratio_lo,
+                           float erase_ratio_hi, uint64_t seed, uint8_t *workspace, float *rgb_out, float *depth_out,
+                           float *depth_raw_out, float *center_out, float *K_out, float *params_out, void *stream);
+
 /* ------------------------------------------------------------------------
  * ResNet50 trunk — replaces torchvision.models.resnet50 children[:-1] as
  * wrapped by every model (pose_net_rgb.py:18-20, pose_net_rgb_geometric.py:18-20,
@@ -219,6 +240,39 @@ int pose6d_conv2d_backward(int32_t dtype, const void *x, const void *dy, const v
                            void *dx, float *dw, int32_t accumulate, float *workspace, int64_t ws_bytes, int32_t N,
                            int32_t H, int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH,
                            int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, void *stream);
+/* Explicit plan overrides for the conv entry points' *_tuned forms -- used by the
+ * tests (every tile / ring depth / kernel of a shape must agree) and the tuning tools,
+ * never by the product path: without one, each conv geometry has exactly one plan,
+ * so one summation order.  Every field -1 = the default plan.
+ *   conv_tile     fast path 0 = 128x128, 1 = 128x64, 3 = 64x64 (4 waves), 4 = 128x128, 5 = 128x64 (8 waves);
+ *                 register-staged path 0..3 = 128x128, 128x64, 64x128, 64x64
+ *   conv_stages   LDS ring slots of the fast path (2, 3, 4, 6)
+ *   conv_s2       0: the stride-2 data gradient as one masked gather instead of 4 parity classes
+ *   conv_base     1: the register-staged conv kernels instead of the LDS-DMA path
+ *   wgrad_stages  LDS ring slots of the bf16 weight-gradient kernel (2..4)
+ *   wgrad_base    1: the register-staged weight-gradient kernel (other split plan)
+ *   bwd_separate  1: data and weight gradient as separate launches (not the fused kernel) */
+typedef struct {
+  int32_t conv_tile, conv_stages, conv_s2, conv_base, wgrad_stages, wgrad_base, bwd_separate;
+} pose6d_tuning_t;
+int pose6d_conv2d_fwd_tuned(int32_t dtype, const void *x, const void *w, const float *bias, void *y, float *stats,
+                            int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW,
+                            int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, const pose6d_tuning_t *tuning,
+                            void *stream);
+int pose6d_conv2d_dgrad_tuned(int32_t dtype, const void *dy, const void *wt, const void *dres, void *dx, int32_t N,
+                              int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
+                              int32_t pad, int32_t Ho, int32_t Wo, const pose6d_tuning_t *tuning, void *stream);
+int64_t pose6d_conv2d_wgrad_workspace_tuned(int32_t dtype, int32_t N, int32_t Ho, int32_t Wo, int32_t Cin,
+                                            int32_t Cout, int32_t KH, int32_t KW, const pose6d_tuning_t *tuning);
+int pose6d_conv2d_wgrad_tuned(int32_t dtype, const void *x, const void *dy, float *dw, int32_t accumulate,
+                              float *workspace, int64_t ws_bytes, int32_t N, int32_t H, int32_t W, int32_t Cin,
+                              int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad,
+                              int32_t Ho, int32_t Wo, const pose6d_tuning_t *tuning, void *stream);
+int pose6d_conv2d_backward_tuned(int32_t dtype, const void *x, const void *dy, const void *wt, const void *dres,
+                                 void *dx, float *dw, int32_t accumulate, float *workspace, int64_t ws_bytes,
+                                 int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout,
+                                 int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
+                                 const pose6d_tuning_t *tuning, void *stream);
 /* pose6d_conv2d_backward in phases (profiling): bit 0 = the gradient launch(es) that
  * fill the fp32 slabs (and dx), bit 1 = the slab reduce into dw; 3 = the whole call.
  * On the unfused path bit 0 runs the complete dgrad + wgrad and bit 1 nothing. */
@@ -227,21 +281,6 @@ int pose6d_conv2d_backward_ex(int32_t dtype, const void *x, const void *dy, cons
                               int32_t H, int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH,
                               int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, int32_t phases,
                               void *stream);
-/* pose6d_conv2d_backward (all phases) whose data-gradient epilogue ALSO produces the
- * BatchNorm-backward partials of the BN that made this conv's input x: dX is that
- * BN's dout, so per 64-pixel tile it writes (sum dz, sum dz * xhat), dz = dout *
- * mask (bn_mk 0: none, 1: out > 0 with bn_out = the BN's forward output, 2:
- * bf16(y * rs + rb) > 0), xhat = (y - mean) * invstd, y = bn_y (the BN's input),
- * into bn_part [2][Cin][bn_rows] for pose6d_bn_bwd_finish.  bf16 fused path only:
- * bn_rows must equal pose6d_conv2d_bn_rows(...) (> 0). */
-int pose6d_conv2d_bn_rows(int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH,
-                          int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo);
-int pose6d_conv2d_backward_bn(int32_t dtype, const void *x, const void *dy, const void *wt, const void *dres,
-                              void *dx, float *dw, int32_t accumulate, float *workspace, int64_t ws_bytes, int32_t N,
-                              int32_t H, int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH,
-                              int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, const void *bn_y,
-                              const void *bn_out, const float *bn_rs, const float *bn_rb, const float *bn_mean,
-                              const float *bn_invstd, float *bn_part, int32_t bn_rows, int32_t bn_mk, void *stream);
 /* Backward chaining across convs: a weight-gradient slab reduce described by
  * pose6d_wgrad_reduce_t (the conv's geometry as passed to pose6d_conv2d_backward,
  * its workspace of slabs and its dW) can ride on the NEXT conv's fused launch as
@@ -325,14 +364,6 @@ int pose6d_bn_bwd(int32_t dtype, const void *dout, const void *out, const float 
                   const float *relu_shift, const void *y, const float *mean, const float *invstd, const float *gamma,
                   float *dgamma, float *dbeta, int32_t accumulate, void *dy, void *dz_out, float *workspace,
                   int64_t M, int32_t C, void *stream);
-
-/* The same backward when the (sum dz, sum dz * xhat) partials already exist, as
- * [2][C][rows] channel-major (pose6d_conv2d_backward_bn wrote them): finalize +
- * apply only.  workspace: 3 * C floats. */
-int pose6d_bn_bwd_finish(int32_t dtype, const void *dout, const void *out, const float *relu_scale,
-                         const float *relu_shift, const void *y, const float *mean, const float *invstd,
-                         const float *gamma, float *dgamma, float *dbeta, int32_t accumulate, void *dy, void *dz_out,
-                         const float *partial, int32_t rows, float *workspace, int64_t M, int32_t C, void *stream);
 
 /* conv bias gradient: out[c] (+)= sum_m x[m][c] over an NHWC tensor of M pixels */
 int pose6d_channel_sum(int32_t dtype, const void *x, int64_t M, int32_t C, float *out, int32_t accumulate,

@@ -152,6 +152,13 @@ def _area2(src):
     return ((s + 2) >> 2).astype(src.dtype)
 
 
+def resized_crop_u8(rgb, bbox_aug, img_size=224):
+    """The uint8 (S, S, 3) crop after cv2.resize: the PIL image the train transform's
+    ColorJitter receives (dataset_rgbd.py:172, 196-197)."""
+    x1, y1, crop, _, _, _, _ = crop_geometry(bbox_aug, rgb.shape[0], rgb.shape[1])
+    return resize_linear_u8(crop_pixels(rgb, x1, y1, crop), img_size)
+
+
 def crop_sample(rgb, depth, bbox_orig, bbox_aug, K, img_size=224, mean=IMAGENET_MEAN, std=IMAGENET_STD):
     """One sample of LineMODDatasetRGBD.__getitem__ after the file reads
     (dataset_rgbd.py:104-206, val transform).  rgb (H, W, 3) uint8 RGB, depth

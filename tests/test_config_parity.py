@@ -278,3 +278,92 @@ def test_configs2_trainer_bs32_bf16_teacher_forced():
                 T.stored(f"conv dgrad:{op.out.name}", _nchw(op.src.g), dx)
     T.check()
     _check_adamw(tr, before)
+
+
+@pytest.mark.gpu
+def test_configs2_eval_forward_bs32_bf16_teacher_forced():
+    """The north-star forward metric's path (bench.py forward_roofline_eval): the
+    PoseNetRGBDGeometric eval forward at batch 32 in bf16 (model.eval(), as the
+    reference's validation loop runs it, train_rgbd_geometric.py:120-136), checked op
+    by op against torch-CPU fp32 ops on the SAME bf16 operands, with non-trivial
+    running statistics.  Covers pose6d_bn_eval_fold (scale / shift from the running
+    statistics), pose6d_conv2d_fwd_act (conv + BN + residual + ReLU in the epilogue),
+    pose6d_conv2d_fwd_act_dual (a downsampling block's conv3 + downsample conv + both
+    BNs in one launch), the stem conv + pose6d_bn_relu_maxpool_fwd, the average pool,
+    and the head's pose6d_gemm_f32_bn_eval; tolerances as the training teacher-forced
+    test above."""
+    from bench import synth_batch
+    from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
+    from pose6d.trunk import _ActOp, _ConvOp, _PoolOp
+    warnings.simplefilter("ignore")
+    torch.manual_seed(0)
+    m = PoseNetRGBDGeometric(pretrained=False)
+    g = torch.Generator().manual_seed(77)
+    for mod in m.modules():
+        if isinstance(mod, (torch.nn.BatchNorm2d, torch.nn.BatchNorm1d)):
+            C = mod.num_features
+            mod.running_mean.copy_(torch.randn(C, generator=g) * 0.1)
+            mod.running_var.copy_(torch.rand(C, generator=g) * 0.5 + 0.5)
+            mod.weight.data.copy_(torch.rand(C, generator=g) + 0.5)
+            mod.bias.data.copy_(torch.randn(C, generator=g) * 0.1)
+    P = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.cuda().set_compute_dtype(torch.bfloat16).eval()
+    rgb, depth_raw, bbox, K, _, _ = synth_batch(32, torch.device("cuda"), seed=4242)
+    with torch.no_grad():
+        rot, trans = m(rgb, None, depth_raw, bbox, K)
+    torch.cuda.synchronize()
+    trunk = m.engines()["backbone"]
+    dual = trunk._dual_pairs()
+    assert dual, "batch 32: the layer1 / layer2 downsampling blocks run as one launch"
+    T = _Tol()
+
+    def bnp(bn):
+        inv = 1.0 / torch.sqrt(bn.running_var.cpu() + bn.eps)
+        sc = bn.weight.detach().cpu() * inv
+        return sc, bn.bias.detach().cpu() - bn.running_mean.cpu() * sc
+
+    def raw(op):   # conv of the stored bf16 input with the bf16 weights, rounded as stored
+        x = _nchw(op.src.t)[:, :op.cin]
+        return F.conv2d(x, op.conv.weight.detach().cpu().bfloat16().float(), None, op.stride,
+                        op.pad).bfloat16().float()
+
+    ref_act = {}
+    for op in trunk.ops:
+        if isinstance(op, _ConvOp):
+            sc, sh = bnp(op.bn)
+            T.sums(f"bn eval fold:{op.out.name}.scale", op.scale.cpu(), sc, 1e-6)
+            T.sums(f"bn eval fold:{op.out.name}.shift", op.shift.cpu(), sh, 1e-6)
+        elif isinstance(op, _ActOp):
+            c = op.cop
+            sc, sh = bnp(c.bn)
+            y = raw(c)
+            if op.pooled:
+                T.stored(f"conv fwd:{c.out.name}", _nchw(c.out.t), y)   # the stem's raw output is stored
+                y = _nchw(c.out.t)
+            z = y * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1)
+            if op.res_conv is not None:
+                r = op.res_conv
+                rs, rb = bnp(r.bn)
+                yr = raw(r) if c in dual else _nchw(r.out.t)
+                if c not in dual:
+                    T.stored(f"conv fwd:{r.out.name}", _nchw(r.out.t), raw(r))
+                z = z + (yr * rs.view(1, -1, 1, 1) + rb.view(1, -1, 1, 1))
+            elif op.res_act is not None:
+                z = z + _nchw(op.res_act.t)
+            if op.relu:
+                z = z.clamp_min(0)
+            ref_act[id(op)] = z
+            if not op.pooled:
+                kind = "fwd act dual" if c in dual else "fwd act"
+                T.stored(f"{kind}:{op.out.name}", _nchw(op.out.t), z)
+        elif isinstance(op, _PoolOp):
+            src = ref_act[id(op.act)].bfloat16().float() if op.act is not None else _nchw(op.src.t)
+            T.stored(f"pool:{op.out.name}", _nchw(op.out.t), F.max_pool2d(src, op.k, op.s, op.p))
+    feat = trunk.feat.detach().cpu()
+    T.sums("avgpool:feat", feat, _nchw(trunk.final.t).mean(dim=(2, 3)), 1e-5)
+    # eval head (Linear + BatchNorm1d + ReLU fused GEMMs) + normalise from our own features
+    ref_rot = OR.normalize(OR.bn_mlp(feat, {k: v for k, v in P.items() if k.startswith("rot_head")}, "rot_head",
+                                     [2048, 1024, 512, 4], False))
+    T.sums("head:rot", rot.cpu(), ref_rot, 1e-4)
+    assert torch.equal(trans.cpu(), OR.pinhole_rgbd_geometric(depth_raw.cpu(), bbox.cpu(), K.cpu()))
+    T.check()

@@ -115,11 +115,12 @@ FAST_CONFIGS = [
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", FAST_CONFIGS)
-def test_conv_fast_variants_bit_identical(cfg, monkeypatch):
+def test_conv_fast_variants_bit_identical(cfg):
     """Every LDS-ring depth / tile of the bf16 fast path (and the parity-class
     stride-2 dgrad vs the masked gather) accumulates each output in the same K
-    order, so all of them must agree bit for bit."""
-    from pose6d._lib import call, stream
+    order, so all of them must agree bit for bit.  The plans are forced through
+    pose6d_tuning_t (the *_tuned entry points); the product calls take none."""
+    from pose6d._lib import Tuning, call, query, stream
     from pose6d.trunk import DTYPES, pack_single
     N, H, W, Cin, Cout, k, s, p = cfg
     g = torch.Generator().manual_seed(7)
@@ -131,49 +132,46 @@ def test_conv_fast_variants_bit_identical(cfg, monkeypatch):
     dres = torch.randn(N, H, W, Cin, generator=g).to(dev, dtype)
     wp, wt = pack_single(w, Cin, dtype)
     dt = DTYPES[dtype]
+    base = Tuning(wgrad_base=1)
+    ws = torch.empty(max(query("conv2d_wgrad_workspace", dt, N, Ho, Wo, Cin, Cout, k, k),
+                         query("conv2d_wgrad_workspace_tuned", dt, N, Ho, Wo, Cin, Cout, k, k, base.ref)) // 4 + 1,
+                     device=dev)
 
-    from pose6d._lib import query
-    ws = torch.empty(query("conv2d_wgrad_workspace", dt, N, Ho, Wo, Cin, Cout, k, k) // 4 + 1, device=dev)
-
-    def run():
+    def run(tn=None):
+        tn = tn if tn is not None else Tuning()
         y = torch.empty(N, Ho, Wo, Cout, device=dev, dtype=dtype)
         dx = torch.empty(N, H, W, Cin, device=dev, dtype=dtype)
         dw = torch.empty(Cout, Cin, k, k, device=dev)
-        call("conv2d_fwd", dt, x, wp, None, y, None, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream())
-        call("conv2d_dgrad", dt, dy, wt, dres, dx, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream())
-        call("conv2d_wgrad", dt, x, dy, dw, 0, ws, ws.numel() * 4, N, H, W, Cin, Cin, Cout, k, k, s, p, Ho, Wo,
-             stream())
+        call("conv2d_fwd_tuned", dt, x, wp, None, y, None, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, tn.ref, stream())
+        call("conv2d_dgrad_tuned", dt, dy, wt, dres, dx, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, tn.ref, stream())
+        call("conv2d_wgrad_tuned", dt, x, dy, dw, 0, ws, ws.numel() * 4, N, H, W, Cin, Cin, Cout, k, k, s, p, Ho, Wo,
+             tn.ref, stream())
         torch.cuda.synchronize()
         return y.cpu(), dx.cpu(), dw.cpu()
 
     y0, dx0, dw0 = run()
-    variants = [{"POSE6D_CONV_STAGES": str(st), "POSE6D_CONV_TILE": str(t)} for st in (2, 3, 4, 6) for t in (0, 1, 3, 4, 5)]
-    variants.append({"POSE6D_CONV_S2": "0"})
-    variants += [{"POSE6D_WGRAD_STAGES": str(st)} for st in (2, 3, 4)]
-    keys = ("POSE6D_CONV_STAGES", "POSE6D_CONV_TILE", "POSE6D_CONV_S2", "POSE6D_WGRAD_STAGES")
-    for env in variants:
-        for key in keys:
-            monkeypatch.delenv(key, raising=False)
-        for key, v in env.items():
-            monkeypatch.setenv(key, v)
-        y1, dx1, dw1 = run()
-        assert torch.equal(y0, y1), f"fwd differs under {env}"
-        assert torch.equal(dx0, dx1), f"dgrad differs under {env}"
-        assert torch.equal(dw0, dw1), f"wgrad differs under {env}"
+    # the plain (untuned) entry points are the default plan
+    y = torch.empty(N, Ho, Wo, Cout, device=dev, dtype=dtype)
+    call("conv2d_fwd", dt, x, wp, None, y, None, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(y.cpu(), y0)
+    variants = [dict(conv_stages=st, conv_tile=t) for st in (2, 3, 4, 6) for t in (0, 1, 3, 4, 5)]
+    variants.append(dict(conv_s2=0))
+    variants += [dict(wgrad_stages=st) for st in (2, 3, 4)]
+    for kw in variants:
+        y1, dx1, dw1 = run(Tuning(**kw))
+        assert torch.equal(y0, y1), f"fwd differs under {kw}"
+        assert torch.equal(dx0, dx1), f"dgrad differs under {kw}"
+        assert torch.equal(dw0, dw1), f"wgrad differs under {kw}"
     # the fused data+weight gradient launch must equal the two separate passes bit for bit
-    for key in keys:
-        monkeypatch.delenv(key, raising=False)
     for sep in (False, True):
-        if sep:
-            monkeypatch.setenv("POSE6D_BWD_SEPARATE", "1")
         dxf = torch.empty(N, H, W, Cin, device=dev, dtype=dtype)
         dwf = torch.empty(Cout, Cin, k, k, device=dev)
-        call("conv2d_backward", dt, x, dy, wt, dres, dxf, dwf, 0, ws, ws.numel() * 4, N, H, W, Cin, Cin, Cout, k, k,
-             s, p, Ho, Wo, stream())
+        call("conv2d_backward_tuned", dt, x, dy, wt, dres, dxf, dwf, 0, ws, ws.numel() * 4, N, H, W, Cin, Cin, Cout,
+             k, k, s, p, Ho, Wo, Tuning(bwd_separate=int(sep)).ref, stream())
         torch.cuda.synchronize()
         assert torch.equal(dxf.cpu(), dx0), f"fused backward dx differs (separate={sep})"
         assert torch.equal(dwf.cpu(), dw0), f"fused backward dw differs (separate={sep})"
-    monkeypatch.delenv("POSE6D_BWD_SEPARATE", raising=False)
     # residual accumulated in place (dres is dx, as the trunk adds the downsample
     # conv's data gradient to conv1's): same bits as the out-of-place sum
     dxi = dres.clone()
@@ -186,11 +184,12 @@ def test_conv_fast_variants_bit_identical(cfg, monkeypatch):
     assert torch.equal(dxi.cpu(), dx0), "in-place backward dx differs"
     assert torch.equal(dxd.cpu(), dx0), "in-place dgrad differs"
     # the register-staged weight gradient sums the pixels in other splits: close, not equal
-    for key in keys:
-        monkeypatch.delenv(key, raising=False)
-    monkeypatch.setenv("POSE6D_WGRAD_IMPL", "base")
-    _, _, dwb = run()
+    _, _, dwb = run(base)
     _close(dwb, dw0, 1e-5, "wgrad base vs LDS-DMA")
+    # the register-staged conv kernels: other K order, close
+    yb, dxb, _ = run(Tuning(conv_base=1))
+    _close(yb, y0, 2e-2, "fwd base vs LDS-DMA")
+    _close(dxb, dx0, 2e-2, "dgrad base vs LDS-DMA")
 
 
 @pytest.mark.gpu
@@ -402,58 +401,3 @@ def test_pack_layouts(dtype, O, I, k, cpad):
     assert torch.equal(wp.float(), full.to(dtype).float())
     if I >= 8:
         assert torch.equal(wt.float(), w.permute(1, 2, 3, 0).to(dtype).float())
-
-
-KG_CONFIGS = [
-    # N, H, W, Cin, Cout, k, s, p: K-steps pair up inside every tap (Cin % 128 for bf16)
-    (2, 14, 14, 128, 128, 1, 1, 0),
-    (2, 14, 14, 128, 64, 3, 1, 1),
-    (2, 28, 28, 256, 128, 3, 2, 1),
-]
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("cfg", KG_CONFIGS)
-def test_conv_fwd_kgroup_tile(cfg, dtype, monkeypatch):
-    """The two-K-group 64x64 tile (POSE6D_CONV_TILE=6; group 1's sums added to group
-    0's in LDS) against the torch fp32 conv, its BN statistics against the batch
-    moments, and its eval BN-act store against y * scale + shift -> ReLU."""
-    from pose6d._lib import call, query, stream
-    from pose6d.trunk import DTYPES, pack_single
-    monkeypatch.setenv("POSE6D_CONV_TILE", "6")
-    N, H, W, Cin, Cout, k, s, p = cfg
-    g = torch.Generator().manual_seed(17)
-    x = torch.randn(N, Cin, H, W, generator=g)
-    w = torch.randn(Cout, Cin, k, k, generator=g) * (2.0 / (Cin * k * k)) ** 0.5
-    if dtype == torch.bfloat16:
-        x = x.bfloat16().float()
-        w = w.bfloat16().float()
-    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
-    dt, dev = DTYPES[dtype], "cuda"
-    xd = _nhwc(x).to(dev, dtype)
-    wp, _ = pack_single(w.to(dev), Cin, dtype, with_t=False)
-    y = torch.empty(N, Ho, Wo, Cout, device=dev, dtype=dtype)
-    rows = query("conv_stats_rows", N, Ho, Wo, Cout)
-    stats = torch.empty(2, Cout, rows, device=dev)
-    call("conv2d_fwd", dt, xd, wp, None, y, stats, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream())
-    yr = F.conv2d(x, w, None, stride=s, padding=p)
-    tol = 1e-4 if dtype == torch.float32 else 2e-2
-    _close(y.permute(0, 3, 1, 2), yr, tol, "fwd (K groups)")
-    C = Cout
-    one, zero = torch.ones(C, device=dev), torch.zeros(C, device=dev)
-    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
-    sc, sh, mu, iv = (torch.empty(C, device=dev) for _ in range(4))
-    ws = torch.empty(64 * 3 * C, device=dev, dtype=torch.float64)
-    call("bn_finalize", stats, rows, C, N * Ho * Wo, one, zero, rm, rv, None, 0.1, 1e-5, 1, sc, sh, mu, iv, ws,
-         stream())
-    _close(mu, yr.double().mean((0, 2, 3)), 1e-4 if dtype == torch.float32 else 1e-2, "batch mean (K groups)")
-    scale = torch.rand(C, device=dev) + 0.5
-    shift = torch.randn(C, device=dev) * 0.1
-    out = torch.empty_like(y)
-    call("conv2d_fwd_act", dt, xd, wp, None, out, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, scale, shift, None, None,
-         None, 1, stream())
-    ref = torch.empty_like(y)   # the separate BN-act launch on the stored conv output
-    call("bn_act_fwd", dt, y, scale, shift, None, None, None, 1, ref, N * Ho * Wo, Cout, stream())
-    torch.cuda.synchronize()
-    assert torch.equal(out, ref)

@@ -116,3 +116,31 @@ def test_geo_head_loss_matches_separate_calls():
     for a, b in ((rot, rot2), (trans, trans2), (loss, loss2), (dtr, dtr2)):
         assert torch.equal(a, b)
     torch.testing.assert_close(draw, draw2, rtol=1e-6, atol=1e-9)
+
+
+def test_eval_head_backward_through_autograd():
+    """Eval-mode head (running-stat BatchNorm1d, no dropout) differentiated through
+    autograd -- e.g. heads fine-tuned under model.eval(): the Linear + BatchNorm1d
+    eval fusion must not run there (grad mode is off inside autograd.Function.forward,
+    yet a backward follows).  Output, input and parameter gradients vs torch fp32."""
+    from pose6d import autograd
+    from pose6d.head import HeadEngine
+    torch.manual_seed(0)
+    seq = torch.nn.Sequential(torch.nn.Linear(256, 128), torch.nn.BatchNorm1d(128), torch.nn.ReLU(),
+                              torch.nn.Dropout(0.3), torch.nn.Linear(128, 4)).cuda().eval()
+    g = torch.Generator().manual_seed(21)
+    bn = seq[1]
+    bn.running_mean.copy_(torch.randn(128, generator=g).cuda() * 0.1)
+    bn.running_var.copy_(torch.rand(128, generator=g).cuda() + 0.5)
+    bn.weight.data.copy_(torch.rand(128, generator=g).cuda() + 0.5)
+    x = torch.randn(32, 256, generator=g).cuda().requires_grad_(True)
+    dy = torch.randn(32, 4, generator=g).cuda()
+    eng = HeadEngine(seq)
+    out = autograd.run(eng, x, False, list(seq.parameters()))
+    grads = torch.autograd.grad(out, [x] + list(seq.parameters()), dy)
+    xr = x.detach().clone().requires_grad_(True)
+    ref = seq(xr)
+    rgrads = torch.autograd.grad(ref, [xr] + list(seq.parameters()), dy)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+    for a, b in zip(grads, rgrads):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5 * b.abs().max().item())

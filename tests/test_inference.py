@@ -41,7 +41,7 @@ def test_b1_eval_forward_and_graph_replay(name):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("name", list(EXPECTED))
-def test_eval_bn_folded_into_conv_is_bit_identical(name, dtype, monkeypatch):
+def test_eval_bn_folded_into_conv_is_bit_identical(name, dtype):
     """Eval forward with BN + residual + ReLU applied in the conv epilogue
     (pose6d_conv2d_fwd_act) equals the separate conv / bn_act launches bit for bit."""
     torch.manual_seed(0)
@@ -49,9 +49,12 @@ def test_eval_bn_folded_into_conv_is_bit_identical(name, dtype, monkeypatch):
     g = torch.Generator().manual_seed(5)
     cin = {k: v.cuda() for k, v in _inputs(2, 224, g).items()}
     outs = []
-    for fold in ("0", "1"):
-        monkeypatch.setenv("POSE6D_EVAL_FUSE", fold)
+    for fold in (False, True):
         with torch.no_grad():
+            _model_forward(name, m, cin)   # creates the engines
+            for eng in m.engines().values():
+                if hasattr(eng, "eval_fuse"):
+                    eng.eval_fuse = fold
             rot, trans = _model_forward(name, m, cin)
         torch.cuda.synchronize()
         outs.append((rot.clone(), trans.clone()))
@@ -59,7 +62,7 @@ def test_eval_bn_folded_into_conv_is_bit_identical(name, dtype, monkeypatch):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_eval_downsample_in_block_launch_is_bit_identical(dtype, monkeypatch):
+def test_eval_downsample_in_block_launch_is_bit_identical(dtype):
     """Eval trunk with each downsampling Bottleneck's conv3 + downsample conv + both
     BatchNorms + add + ReLU in ONE launch (pose6d_conv2d_fwd_act_dual) equals the
     separate downsample launch + fused conv3 epilogue bit for bit (all four stages:
@@ -80,13 +83,10 @@ def test_eval_downsample_in_block_launch_is_bit_identical(dtype, monkeypatch):
     eng = TrunkEngine(seq, 3)
     eng.set_dtype(dtype)
     x = torch.randn(4, 3, 224, 224, generator=g).cuda()
-    monkeypatch.setenv("POSE6D_EVAL_DUAL_ROWS", "0")   # every stage (batch 4 grids are small)
-    # the one-launch kernel sums like the 4-wave 64x64 tile; pin the separate launches to it
-    # (the K-group tile some small grids pick sums in another order)
-    monkeypatch.setenv("POSE6D_CONV_TILE", "3")
+    eng.eval_dual_rows = 0   # every stage (batch 4 grids are small: the default tile is 64x64 too)
     feats = []
-    for dual in ("0", "1"):
-        monkeypatch.setenv("POSE6D_EVAL_DUAL", dual)
+    for dual in (False, True):
+        eng.eval_dual = dual
         with torch.no_grad():
             feats.append(eng.forward(x, False).clone())
         torch.cuda.synchronize()
@@ -95,7 +95,7 @@ def test_eval_downsample_in_block_launch_is_bit_identical(dtype, monkeypatch):
 
 
 @pytest.mark.parametrize("name", list(EXPECTED))
-def test_eval_head_linear_bn1d_fused_is_bit_identical(name, monkeypatch):
+def test_eval_head_linear_bn1d_fused_is_bit_identical(name):
     """Eval heads: each Linear -> BatchNorm1d (+ ReLU) pair as one GEMM with the BN in
     its store (pose6d_gemm_f32_bn_eval) equals the separate launches bit for bit,
     with non-trivial running statistics."""
@@ -110,10 +110,15 @@ def test_eval_head_linear_bn1d_fused_is_bit_identical(name, monkeypatch):
             mod.weight.data.copy_(torch.rand(C, generator=g) + 0.5)
     m = m.cuda().eval()
     cin = {k: v.cuda() for k, v in _inputs(8, 224, g).items()}
+    from pose6d.head import HeadEngine
     outs = []
-    for fuse in ("0", "1"):
-        monkeypatch.setenv("POSE6D_HEAD_BN_FUSE", fuse)
+    for fuse in (False, True):
         with torch.no_grad():
+            _model_forward(name, m, cin)   # creates the engines
+            heads = [e for e in m.engines().values() if isinstance(e, HeadEngine)]
+            assert heads
+            for e in heads:
+                e.fuse_eval_bn = fuse
             rot, trans = _model_forward(name, m, cin)
         torch.cuda.synchronize()
         outs.append((rot.clone(), trans.clone()))

@@ -1,6 +1,8 @@
 """Per-layer conv timing sweep (GPU box): every distinct ResNet50 conv shape at
 batch 32 bf16, fwd / dgrad / wgrad, each implementation x tile, TFLOP/s.
-usage: python tools/conv_bench.py [--passes fwd,dgrad] [--impls base,fast] [--tiles 0,1,2,3]"""
+usage: python tools/conv_bench.py [--passes fwd,dgrad] [--impls base,fast] [--tiles 0,1,2,3]
+Plans are chosen through pose6d_tuning_t (the *_tuned entry points); --env / --wgrad-env
+sweep tuning fields, e.g. --env "conv_tile=4,conv_stages=2;conv_s2=0"."""
 import argparse
 import os
 import sys
@@ -11,7 +13,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "6d-pose-estimation_amd")]
 
 import pose6d._lib as _plib  # noqa: E402
-from pose6d._lib import call, query, stream  # noqa: E402
+from pose6d._lib import Tuning, call, query, stream  # noqa: E402
 from pose6d.trunk import DTYPES, pack_single  # noqa: E402
 
 # (H, W, Cin, Cout, k, s, p) per distinct ResNet50 conv (input geometry)
@@ -28,6 +30,14 @@ SHAPES = [
 
 
 GRAPH = False
+TUNE = Tuning()   # the plan override the timed calls pass (mutated by the sweeps)
+
+
+def _set_tune(**kw):
+    for f, _ in Tuning._fields_:
+        setattr(TUNE, f, -1)
+    for k, v in kw.items():
+        setattr(TUNE, k, int(v))
 
 
 def timeit(fn, reps=20):
@@ -63,8 +73,10 @@ def main():
     ap.add_argument("--impls", default="base,fast")
     ap.add_argument("--tiles", default="auto,0,1,3")
     ap.add_argument("--stages", default="auto", help="fast-path LDS ring depths to sweep, e.g. auto,2,3,4,6")
-    ap.add_argument("--wgrad-env", default="", help="';'-separated K=V[,K=V] settings to sweep for wgrad")
-    ap.add_argument("--env", default="", help="';'-separated K=V[,K=V] settings to sweep for fwd / dgrad")
+    ap.add_argument("--wgrad-env", default="", help="';'-separated field=V[,field=V] pose6d_tuning_t settings to "
+                                                     "sweep for wgrad")
+    ap.add_argument("--env", default="", help="';'-separated field=V[,field=V] pose6d_tuning_t settings to sweep "
+                                           "for fwd / dgrad")
     ap.add_argument("--B", type=int, default=32)
     ap.add_argument("--only", default="", help="comma-separated indices into SHAPES")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
@@ -90,14 +102,16 @@ def main():
         dx = torch.empty(B, H, W, Cin, device=dev, dtype=dtype)
         stats = torch.empty(query("conv_stats_rows", B, Ho, Wo, Cout), 2, Cout, device=dev)
         # room for any split plan the --wgrad-env sweep selects (the call checks the size)
-        ws = torch.empty(max(query("conv2d_wgrad_workspace", dt, B, Ho, Wo, Cin, Cout, k, k), 256 << 20) // 4,
+        ws = torch.empty(max(query("conv2d_wgrad_workspace_tuned", dt, B, Ho, Wo, Cin, Cout, k, k,
+                                   Tuning(wgrad_base=1).ref), 256 << 20) // 4,
                          device=dev)
         dw = torch.empty(Cout, Cin, k, k, device=dev)
         flops = 2.0 * B * Ho * Wo * Cout * Cin * k * k
         sc, sh = torch.rand(Cout, device=dev) + 0.5, torch.randn(Cout, device=dev) * 0.1
         res = torch.randn(B, Ho, Wo, Cout, device=dev).to(dtype) if "fwdactres" in a.passes else None
         fns = {
-            "fwd": lambda: call("conv2d_fwd", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream()),
+            "fwd": lambda: call("conv2d_fwd_tuned", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k, k, s, p, Ho,
+                                Wo, TUNE.ref, stream()),
             # no BN statistics (as in eval without the fold)
             "fwdns": lambda: call("conv2d_fwd", dt, x, wp, None, y, None, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo,
                                   stream()),
@@ -110,14 +124,15 @@ def main():
                                    sh, None, None, None, 1, stream()),
             "fwdactres": lambda: call("conv2d_fwd_act", dt, x, wp, None, y, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo,
                                       sc, sh, res, None, None, 1, stream()),
-            "dgrad": lambda: call("conv2d_dgrad", dt, dy, wt, None, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream()),
+            "dgrad": lambda: call("conv2d_dgrad_tuned", dt, dy, wt, None, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo,
+                                  TUNE.ref, stream()),
             "dgradip": lambda: call("conv2d_dgrad", dt, dy, wt, dx, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream()),
             "bwdip": lambda: call("conv2d_backward", dt, x, dy, wt, dx, dx, dw, 0, ws, ws.numel() * 4, B, H, W, Cin,
                                   Cin, Cout, k, k, s, p, Ho, Wo, stream()),
-            "bwd": lambda: call("conv2d_backward", dt, x, dy, wt, None, dx, dw, 0, ws, ws.numel() * 4, B, H, W, Cin,
-                                Cin, Cout, k, k, s, p, Ho, Wo, stream()),
-            "wgrad": lambda: call("conv2d_wgrad", dt, x, dy, dw, 0, ws, ws.numel() * 4, B, H, W, Cin, Cin, Cout, k, k,
-                                  s, p, Ho, Wo, stream()),
+            "bwd": lambda: call("conv2d_backward_tuned", dt, x, dy, wt, None, dx, dw, 0, ws, ws.numel() * 4, B, H, W,
+                                Cin, Cin, Cout, k, k, s, p, Ho, Wo, TUNE.ref, stream()),
+            "wgrad": lambda: call("conv2d_wgrad_tuned", dt, x, dy, dw, 0, ws, ws.numel() * 4, B, H, W, Cin, Cin, Cout,
+                                  k, k, s, p, Ho, Wo, TUNE.ref, stream()),
         }
         line = f"{H:3d}x{W:<3d} {Cin:4d}->{Cout:<4d} k{k}s{s} |"
         if "fwdcold" in a.passes.split(","):
@@ -129,11 +144,9 @@ def main():
             if sweep:
                 for spec in ["auto"] + sweep.split(";"):
                     kv = [] if spec == "auto" else [e.split("=") for e in spec.split(",")]
-                    for k_, v_ in kv:
-                        os.environ[k_] = v_
+                    _set_tune(**{k_: v_ for k_, v_ in kv})
                     sec = timeit(fns[ps])
-                    for k_, _ in kv:
-                        os.environ.pop(k_, None)
+                    _set_tune()
                     line += f" {ps[0]}[{spec}]:{sec * 1e6:6.1f}us/{flops / sec / 1e12:5.0f}T"
                 continue
             impls = {"wgrad": ["base"], "bwd": ["fast"], "bwdip": ["fast"]}.get(ps, a.impls.split(","))
@@ -142,12 +155,12 @@ def main():
                 stages = a.stages.split(",") if impl == "fast" else ["auto"]
                 for t in tiles:
                     for nst in stages:
-                        os.environ["POSE6D_CONV_IMPL"] = impl
-                        for key, val in (("POSE6D_CONV_TILE", t), ("POSE6D_CONV_STAGES", nst)):
-                            if val == "auto":
-                                os.environ.pop(key, None)
-                            else:
-                                os.environ[key] = val
+                        kw = {"conv_base": int(impl == "base"), "wgrad_base": int(impl == "base")}
+                        if t != "auto":
+                            kw["conv_tile"] = t
+                        if nst != "auto":
+                            kw["conv_stages"] = nst
+                        _set_tune(**kw)
                         try:
                             sec = timeit(fns[ps])
                         except Exception as e:  # noqa: BLE001
@@ -158,8 +171,7 @@ def main():
                         line += f" {tag}:{sec * 1e6:6.1f}us/{tf:5.0f}T"
                         if t == "auto" and nst == "auto":
                             tot[(ps, impl)] = tot.get((ps, impl), 0.0) + sec
-        for key in ("POSE6D_CONV_IMPL", "POSE6D_CONV_TILE", "POSE6D_CONV_STAGES"):
-            os.environ.pop(key, None)
+        _set_tune()
         print(line, flush=True)
     print("totals (auto tile, one instance per distinct shape):",
           {f"{k[0]}/{k[1]}": round(v * 1e3, 3) for k, v in tot.items()})

@@ -1,5 +1,5 @@
 """Eval-mode forward time at bs32 (bf16 and fp32), with and without the BN folded into the
-conv epilogues (POSE6D_EVAL_FUSE): usage python tools/eval_fwd.py"""
+conv epilogues (TrunkEngine.eval_fuse): usage python tools/eval_fwd.py"""
 import os
 import sys
 
@@ -18,9 +18,12 @@ def main():
     args = (b[0], None, b[1], b[2], b[3])
     for dt in (torch.bfloat16, torch.float32):
         m = PoseNetRGBDGeometric(pretrained=False).to(dev).set_compute_dtype(dt).eval()
-        for fold in ("0", "1"):
-            os.environ["POSE6D_EVAL_FUSE"] = fold
+        for fold in (False, True):
             with torch.no_grad():
+                m(*args)
+                for eng in m.engines().values():
+                    if hasattr(eng, "eval_fuse"):
+                        eng.eval_fuse = fold
                 t = _time_fn(lambda: m(*args), 20)
             print(f"{dt} fold={fold}: {t * 1e3:.3f} ms/batch  {32 / t:.0f} crops/s", flush=True)
 
