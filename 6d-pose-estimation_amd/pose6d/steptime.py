@@ -11,9 +11,13 @@ While the step is captured, every pose6d entry point called (pose6d._lib.call) i
 logged with the graph's node count after it, so each kernel node maps back to the
 call (and conv geometry) that launched it: that gives algorithmic flops per node.
 
-Used by bench.py for the `roofline` object and the per-symbol breakdown; rocprofv3
---kernel-trace of the normal (uninstrumented) replay is the cross-check
-(profiles/r03*_step_trace*).
+Each event node adds a nearly constant cost to the interval it closes (the marker
+packet between two dispatches: ~3 us on MI355X).  run(plain_ms=...) calibrates it
+against the uninstrumented replay of the same step: overhead per node = (instrumented
+step - plain step) / nodes, subtracted from every node.  With it the in-step averages
+agree with rocprofv3 --kernel-trace of the plain replay within ~1 % (profiles/r03*).
+
+Used by bench.py for the `roofline` object and the per-symbol breakdown.
 """
 import collections
 import ctypes
@@ -78,6 +82,10 @@ def short_name(mangled):
         _demangle.restype = ctypes.c_void_p
     st = ctypes.c_int(0)
     p = _demangle(mangled, None, None, ctypes.byref(st))
+    if (st.value != 0 or not p) and b"DF16b" in mangled:
+        # libstdc++ 11 does not know the __bf16 mangling (DF16b): spell it as the
+        # vendor type u6__bf16, which demangles to "__bf16" with the same substitutions
+        p = _demangle(mangled.replace(b"DF16b", b"u6__bf16"), None, None, ctypes.byref(st))
     if st.value != 0 or not p:
         return mangled.decode()
     s = ctypes.string_at(p).decode()
@@ -149,19 +157,32 @@ def conv_flops(name, args, sym):
         N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo = args[6:17] if name == "conv2d_fwd" else args[5:16]
         cin = 3 if Cin == 4 else Cin   # the padded stem input (RGB padded to 4 channels)
         return 2.0 * N * Ho * Wo * Cout * KH * KW * cin
-    if name in ("conv2d_backward_chain", "conv2d_backward_chain_masked", "conv2d_backward_bn"):
+    if name in ("conv2d_backward_chain", "conv2d_backward_chain_masked"):
         i0 = 11 if name == "conv2d_backward_chain_masked" else 10
         N, H, W, Cin, Cin_real, Cout, KH, KW, stride, pad, Ho, Wo = args[i0:i0 + 12]
         one = 2.0 * N * Ho * Wo * Cout * KH * KW * Cin_real
         if sym.startswith("conv_bwd_kernel"):
             return 2 * one          # data + weight gradient in one launch
-        if not args[i0 - 5]:        # dx == NULL: weight gradient only (the stem)
+        if args[i0 - 5] is None:    # dx == NULL: weight gradient only (the stem)
             return one if "wgrad" in sym else 0.0
         return one                  # a separate data-gradient or weight-gradient launch
     if name == "conv2d_fwd_act_dual":
         N, Ho, Wo, Cin, Cout, Hd, Wd, Cind = args[6:14]
         return 2.0 * N * Ho * Wo * Cout * (Cin + Cind)
     return None
+
+
+def conv_geom(name, args):
+    """'N HxW Cin->Cout kKsS' of a conv call (None otherwise), for per-launch listings."""
+    idx = {"conv2d_fwd": 6, "conv2d_fwd_act": 5, "conv2d_backward_chain": 10, "conv2d_backward_chain_masked": 11}
+    if name not in idx:
+        return None
+    i = idx[name]
+    if name.startswith("conv2d_backward"):
+        N, H, W, Cin, _, Cout, KH, _, stride = args[i:i + 9]
+    else:
+        N, H, W, Cin, Cout, KH, _, stride = args[i:i + 8]
+    return f"{N} {H}x{W} {Cin}->{Cout} k{KH}s{stride}"
 
 
 class StepTimer:
@@ -218,7 +239,8 @@ class StepTimer:
                 sym = short_name(nm) if nm else "?"
             name, args = owner[i] if owner[i] else (None, None)
             fl = conv_flops(name, args, sym) if (sym and name) else None
-            self.records.append({"node": i, "type": t.value, "kernel": sym, "call": name, "flops": fl})
+            self.records.append({"node": i, "type": t.value, "kernel": sym, "call": name, "flops": fl,
+                                 "geom": conv_geom(name, args) if name else None})
             # splice: deps(node) -> event_i -> node
             ev = ctypes.c_void_p()
             if i == 0:
@@ -237,8 +259,10 @@ class StepTimer:
         self.graph.instantiate()
         self.stream = s
 
-    def run(self, reps=10):
-        """Replay `reps` times; each kernel record gets 'us' = mean in-step duration."""
+    def run(self, reps=10, plain_ms=None):
+        """Replay `reps` times; each kernel record gets 'us' = mean in-step duration
+        (minus the calibrated per-node event overhead when `plain_ms`, the step's
+        uninstrumented replay time, is given) and 'us_raw' = the raw event interval."""
         h = hip()
         n = len(self.records)
         acc = [0.0] * n
@@ -254,9 +278,13 @@ class StepTimer:
                 acc[i] += ms.value
             _ok(h.hipEventElapsedTime(ctypes.byref(ms), self.events[0], self.events[n]), "elapsed")
             total += ms.value
-        for r, a in zip(self.records, acc):
-            r["us"] = a / reps * 1e3
         self.total_ms = total / reps
+        self.overhead_us = 0.0
+        if plain_ms is not None and plain_ms < self.total_ms:
+            self.overhead_us = (self.total_ms - plain_ms) * 1e3 / n
+        for r, a in zip(self.records, acc):
+            r["us_raw"] = a / reps * 1e3
+            r["us"] = max(r["us_raw"] - self.overhead_us, 0.0)
         return [r for r in self.records if r["type"] == 0]
 
     def close(self):
@@ -270,9 +298,11 @@ def by_symbol(records):
     """{kernel symbol: {launches, time_us, flops}} over kernel records, by total time."""
     agg = collections.OrderedDict()
     for r in records:
-        a = agg.setdefault(r["kernel"], {"launches": 0, "time_us": 0.0, "flops": 0.0, "flops_known": True})
+        a = agg.setdefault(r["kernel"], {"launches": 0, "time_us": 0.0, "time_raw_us": 0.0, "flops": 0.0,
+                                         "flops_known": True})
         a["launches"] += 1
         a["time_us"] += r["us"]
+        a["time_raw_us"] += r.get("us_raw", r["us"])
         if r["flops"] is None:
             a["flops_known"] = False
         else:

@@ -274,7 +274,7 @@ def kernel_profile(tr, data, step_ms, peak_tflops=None, with_forward=True, reps=
     if peak_tflops is None:
         peak_tflops = PEAK_BF16_TFLOPS if tr.trunk.dtype == torch.bfloat16 else PEAK_F32_MFMA_TFLOPS
     timer = steptime.StepTimer(lambda: tr.step_body(data), tr.dev)
-    recs = timer.run(reps)
+    recs = timer.run(reps, plain_ms=step_ms)
     inst_ms = timer.total_ms
     timer.close()
     agg = steptime.by_symbol(recs)
@@ -297,9 +297,15 @@ def kernel_profile(tr, data, step_ms, peak_tflops=None, with_forward=True, reps=
                      "avg_launch_us": round(avg_t * 1e6, 2),
                      "algorithmic_flops_per_launch": a["flops"] / a["launches"],
                      "timing": "in-step: HIP event nodes spliced around every kernel node of the captured step "
-                               f"graph (pose6d/steptime.py), mean over {reps} replays"},
+                               f"graph (pose6d/steptime.py), mean over {reps} replays, minus the calibrated event-node "
+                               f"overhead ({timer.overhead_us:.2f} us/node = (instrumented - plain step) / nodes)",
+                     "avg_launch_us_raw_events": round(a["time_raw_us"] / a["launches"], 2),
+                     "per_launch": [[r["geom"], round(r["us"], 2),
+                                     round(r["flops"] / (r["us"] * 1e-6) / 1e12, 1) if r["us"] > 0 else None]
+                                    for r in recs if r["kernel"] == sym]},
         "breakdown": {"kernels_per_step": len(recs), "gpu_busy_ms_per_step": round(busy_ms, 3),
                       "instrumented_step_ms": round(inst_ms, 3), "step_ms": round(step_ms, 3),
+                      "event_overhead_us_per_node": round(timer.overhead_us, 3),
                       "conv_kernels_ms_per_step": round(conv_total_ms, 3),
                       "by_symbol": {k: {"launches": v["launches"], "ms": round(v["time_us"] * 1e-3, 4),
                                         "avg_us": round(v["time_us"] / v["launches"], 2),

@@ -85,7 +85,8 @@ def _run(aug, B=32, seed=0):
     crop = CropRGBD(224, augment=aug)
     out = crop(d(rgb), d(depth), d(bb), d(bb), d(K))
     torch.cuda.synchronize()
-    return rgb, bb, [o.cpu().numpy() for o in out], crop.last_params.cpu().numpy()
+    params = crop.last_params.cpu().numpy() if crop.last_params is not None else None
+    return rgb, bb, [o.cpu().numpy() for o in out], params
 
 
 def _replay(rgb, bb, params, i):

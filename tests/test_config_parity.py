@@ -148,11 +148,15 @@ class _Tol:
     def __init__(self):
         self.worst = {}
 
-    def stored(self, what, got, ref):
-        # a bf16 tensor that should be bf16(ref): one bf16 ulp + 1e-3 of the RMS
+    def stored(self, what, got, ref, extra=None):
+        # a bf16 tensor that should be bf16(ref): one bf16 ulp + 1e-3 of the RMS (+ `extra`:
+        # an elementwise allowance for intermediates rounded to bf16 inside the kernel)
         got, ref = got.double(), ref.double()
         rms = ref.pow(2).mean().sqrt().item() + 1e-30
-        r = ((got - ref).abs() / (2.0 ** -7 * ref.abs() + 1e-3 * rms)).max().item()
+        tol = 2.0 ** -7 * ref.abs() + 1e-3 * rms
+        if extra is not None:
+            tol = tol + extra.double()
+        r = ((got - ref).abs() / tol).max().item()
         self._put(what, r)
 
     def sums(self, what, got, ref, tol=1e-3):
@@ -341,12 +345,18 @@ def test_configs2_eval_forward_bs32_bf16_teacher_forced():
                 T.stored(f"conv fwd:{c.out.name}", _nchw(c.out.t), y)   # the stem's raw output is stored
                 y = _nchw(c.out.t)
             z = y * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1)
+            # the fused epilogue rounds the conv accumulator to bf16 before the BN, as the
+            # separate launches' stored output was: that rounding may land one bf16 ulp
+            # away from bf16(our fp32 conv) (other summation order), scaled by the BN
+            flip = 2.0 ** -7 * y.abs() * sc.abs().view(1, -1, 1, 1) if not op.pooled else None
             if op.res_conv is not None:
                 r = op.res_conv
                 rs, rb = bnp(r.bn)
                 yr = raw(r) if c in dual else _nchw(r.out.t)
                 if c not in dual:
                     T.stored(f"conv fwd:{r.out.name}", _nchw(r.out.t), raw(r))
+                else:
+                    flip = flip + 2.0 ** -7 * yr.abs() * rs.abs().view(1, -1, 1, 1)
                 z = z + (yr * rs.view(1, -1, 1, 1) + rb.view(1, -1, 1, 1))
             elif op.res_act is not None:
                 z = z + _nchw(op.res_act.t)
@@ -355,7 +365,7 @@ def test_configs2_eval_forward_bs32_bf16_teacher_forced():
             ref_act[id(op)] = z
             if not op.pooled:
                 kind = "fwd act dual" if c in dual else "fwd act"
-                T.stored(f"{kind}:{op.out.name}", _nchw(op.out.t), z)
+                T.stored(f"{kind}:{op.out.name}", _nchw(op.out.t), z, flip)
         elif isinstance(op, _PoolOp):
             src = ref_act[id(op.act)].bfloat16().float() if op.act is not None else _nchw(op.src.t)
             T.stored(f"pool:{op.out.name}", _nchw(op.out.t), F.max_pool2d(src, op.k, op.s, op.p))
