@@ -89,7 +89,13 @@ class RGBDGeometricTrainer:
         self.v = torch.zeros_like(self.arena.flat)
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
         # hp[6]: gradient scale read by adamw_step -- 1/world averages the all-reduced sum
-        self.hp = torch.tensor([lr, betas[0], betas[1], eps, weight_decay, 0.0, 1.0 / self.world, max_norm],
+        # inside the update (exact for power-of-two world sizes: scaling by 2^-k commutes
+        # with every rounding; arena.grad then holds the SUM after a step).  Other world
+        # sizes average the gradient in a pass of their own first, as torch DDP does
+        # (g_sum * (1/world) rounded once, then clipped), and hp[6] stays 1.
+        self._avg_pass = self.world > 1 and (self.world & (self.world - 1)) != 0
+        scale = 1.0 if (self.world == 1 or self._avg_pass) else 1.0 / self.world
+        self.hp = torch.tensor([lr, betas[0], betas[1], eps, weight_decay, 0.0, scale, max_norm],
                                device=dev, dtype=torch.float32)
         self.partials = torch.zeros(NPART, device=dev)
         self.norm = torch.zeros(1, device=dev)
@@ -135,6 +141,8 @@ class RGBDGeometricTrainer:
 
     def _optimizer(self):
         st = stream()
+        if self._avg_pass:
+            self.arena.grad.mul_(1.0 / self.world)   # torch DDP's average (non power-of-two world)
         # (world > 1: the 1/world average of the all-reduced gradient is hp[6], applied
         # inside adamw_step; the norm partials see the sum, scaled there too)
         # step counter hp[5] += 1 and dropout seed += 1 ride on the norm-partials launch

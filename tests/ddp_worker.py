@@ -1,5 +1,6 @@
-"""Worker of tests/test_ddp_gpu.py (launched by torch.distributed.run, 2 ranks on
-ONE GPU over gloo: RCCL needs a GPU per rank).  Each rank trains one step on its
+"""Worker of tests/test_ddp_gpu.py (launched by torch.distributed.run, 2 or 3 ranks on
+ONE GPU over gloo: RCCL needs a GPU per rank; 3 ranks exercise the non-power-of-two
+average pass).  Each rank trains one step on its
 OWN batch (seed 77 + rank) through the bucketed all-reduce path
 (RGBDGeometricTrainer with a process group), eagerly and replayed from the
 segmented graphs.  Rank 0 also builds the expected update in one process: the
@@ -74,12 +75,21 @@ def main():
         grads.append(t.arena.grad.clone())
     t = trainer(None)
     with torch.no_grad():
-        t.arena.grad.copy_(grads[0] + grads[1])
+        total = grads[0].clone()
+        for g in grads[1:]:
+            total += g
+        t.arena.grad.copy_(total)
         t.arena.grad.mul_(1.0 / world)
     t._optimizer()
     torch.cuda.synchronize()
     flat_ref = t.arena.flat
-    res = [int(torch.equal(flat_eager, flat_ref)), float((flat_eager - flat_ref).abs().max()),
+    # two ranks: the all-reduce sum is exact, so bit for bit; more ranks: gloo's summation
+    # order may differ from this left-to-right sum by an ulp, then ~1e-4 relative after AdamW
+    if world == 2:
+        same = torch.equal(flat_eager, flat_ref)
+    else:
+        same = bool(((flat_eager - flat_ref).abs() <= 1e-7 + 1e-4 * flat_ref.abs()).all())
+    res = [int(same), float((flat_eager - flat_ref).abs().max()),
            int(torch.equal(flat_graph, flat_eager)), int(torch.equal(run_eager, run_ref)),
            int(torch.equal(run_graph, run_ref)), int(ranks_agree), n_buckets, n_segs,
            int(not torch.equal(grads[0], grads[1]))]
