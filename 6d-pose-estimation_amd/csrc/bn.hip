@@ -243,7 +243,10 @@ __device__ __forceinline__ void relu_mask(float (&d)[V<T>::E], const uint4& ov, 
   }
 }
 
-template <typename T, int MK>
+// DUAL: a second BatchNorm fed by the same dout + mask (a downsampling block's
+// branch BN: y2 / mean2 / inv2 -> part2), summed in the same pass -- sum dz is shared,
+// sum dz * xhat2 is its own; each BN's sums are the single-BN kernel's, bit for bit
+template <typename T, int MK, bool DUAL = false>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce2_kernel(const T* __restrict__ dout, const T* __restrict__ out,
                                                                   const float* __restrict__ rs,
                                                                   const float* __restrict__ rb,
@@ -251,17 +254,25 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce2_kernel(const T* __res
                                                                   const float* __restrict__ mean,
                                                                   const float* __restrict__ inv,
                                                                   float* __restrict__ part, int64_t M, int C,
-                                                                  int rows_per_block) {
+                                                                  int rows_per_block, const T* __restrict__ y2 = nullptr,
+                                                                  const float* __restrict__ mean2 = nullptr,
+                                                                  const float* __restrict__ inv2 = nullptr,
+                                                                  float* __restrict__ part2 = nullptr) {
   constexpr int E = V<T>::E;
-  __shared__ float sred[kThreads][2 * E + 1];
+  __shared__ float sred[kThreads][(DUAL ? 3 : 2) * E + 1];
   const int cpr = C / E;
   const int CL = cpr < 64 ? cpr : 64, RL = kThreads / CL;
   const int cl = threadIdx.x % CL, rl = threadIdx.x / CL;
   const int ch = blockIdx.x * CL + cl;
   const int c0 = ch * E;
   float s[E], q[E], mu[E], iv[E];
+  float q2[DUAL ? E : 1], mu2[DUAL ? E : 1], iv2[DUAL ? E : 1];
 #pragma unroll
   for (int e = 0; e < E; ++e) { s[e] = q[e] = 0.f; mu[e] = mean[c0 + e]; iv[e] = inv[c0 + e]; }
+  if constexpr (DUAL) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) { q2[e] = 0.f; mu2[e] = mean2[c0 + e]; iv2[e] = inv2[c0 + e]; }
+  }
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
   const int64_t r1 = min(M, r0 + rows_per_block);
   // U rows per trip with every load issued before any use: 3 * U 16-byte loads in
@@ -269,7 +280,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce2_kernel(const T* __res
   constexpr int U = 4;
   int64_t r = r0 + rl;
   for (; r + (U - 1) * RL < r1; r += U * RL) {
-    uint4 dv[U], ov[U], yv[U];
+    uint4 dv[U], ov[U], yv[U], y2v[DUAL ? U : 1];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t off = (r + u * RL) * C + c0;
@@ -277,6 +288,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce2_kernel(const T* __res
       if constexpr (MK == 1) ov[u] = *reinterpret_cast<const uint4*>(out + off);
       if constexpr (MK == 3) ov[u].x = reinterpret_cast<const uint8_t*>(out)[off / E];
       yv[u] = *reinterpret_cast<const uint4*>(y + off);
+      if constexpr (DUAL) y2v[u] = *reinterpret_cast<const uint4*>(y2 + off);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -288,6 +300,12 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce2_kernel(const T* __res
       for (int e = 0; e < E; ++e) {
         s[e] += d[e];
         q[e] = fmaf(d[e], (yy[e] - mu[e]) * iv[e], q[e]);
+      }
+      if constexpr (DUAL) {
+        float y2f[E];
+        load_vec(reinterpret_cast<const T*>(&y2v[u]), y2f);
+#pragma unroll
+        for (int e = 0; e < E; ++e) q2[e] = fmaf(d[e], (y2f[e] - mu2[e]) * iv2[e], q2[e]);
       }
     }
   }
@@ -305,15 +323,29 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce2_kernel(const T* __res
       s[e] += d[e];
       q[e] = fmaf(d[e], (yy[e] - mu[e]) * iv[e], q[e]);
     }
+    if constexpr (DUAL) {
+      float y2f[E];
+      load_vec(y2 + off, y2f);
+#pragma unroll
+      for (int e = 0; e < E; ++e) q2[e] = fmaf(d[e], (y2f[e] - mu2[e]) * iv2[e], q2[e]);
+    }
   }
 #pragma unroll
   for (int e = 0; e < E; ++e) { sred[threadIdx.x][e] = s[e]; sred[threadIdx.x][E + e] = q[e]; }
+  if constexpr (DUAL) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) sred[threadIdx.x][2 * E + e] = q2[e];
+  }
   __syncthreads();
   if (rl == 0) {
     for (int k = 1; k < RL; ++k) {
       const int t = k * CL + cl;
 #pragma unroll
       for (int e = 0; e < E; ++e) { s[e] += sred[t][e]; q[e] += sred[t][E + e]; }
+      if constexpr (DUAL) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) q2[e] += sred[t][2 * E + e];
+      }
     }
     // channel-major partials [2][C][row blocks] (coalesced reads in the finalize)
     const int64_t nrb = gridDim.y;
@@ -321,15 +353,31 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce2_kernel(const T* __res
     for (int e = 0; e < E; ++e) {
       part[(int64_t)(c0 + e) * nrb + blockIdx.y] = s[e];
       part[((int64_t)C + c0 + e) * nrb + blockIdx.y] = q[e];
+      if constexpr (DUAL) {
+        part2[(int64_t)(c0 + e) * nrb + blockIdx.y] = s[e];
+        part2[((int64_t)C + c0 + e) * nrb + blockIdx.y] = q2[e];
+      }
     }
   }
 }
+
+struct BwdFin {   // one BatchNorm's finalize operands (grid.y picks one of two)
+  const float* part;
+  const float* gamma;
+  const float* inv;
+  float *dgamma, *dbeta, *coef;
+};
 
 __global__ __launch_bounds__(kThreads) void bn_bwd_finalize_kernel(const float* __restrict__ part, int rows, int C,
                                                                    double count, const float* __restrict__ gamma,
                                                                    const float* __restrict__ inv,
                                                                    float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                                   int accumulate, float* __restrict__ coef) {
+                                                                   int accumulate, float* __restrict__ coef,
+                                                                   BwdFin second_v = BwdFin{}) {
+  if (blockIdx.y == 1) {   // the second BatchNorm of a dual backward
+    part = second_v.part; gamma = second_v.gamma; inv = second_v.inv;
+    dgamma = second_v.dgamma; dbeta = second_v.dbeta; coef = second_v.coef;
+  }
   // one wave per channel: lanes read the channel's partial rows coalesced
   // (channel-major [2][C][rows]), fp64 sums combined by a fixed xor tree
   const int lane = threadIdx.x & 63;
@@ -369,14 +417,19 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_finalize_kernel(const float* 
   }
 }
 
-template <typename T, int MK>
+template <typename T, int MK, bool DUAL = false>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const T* __restrict__ dout, const T* __restrict__ out,
                                                                 const float* __restrict__ rs,
                                                                 const float* __restrict__ rb,
                                                                 const T* __restrict__ y, const float* __restrict__ mean,
                                                                 const float* __restrict__ inv,
                                                                 const float* __restrict__ coef, T* __restrict__ dy,
-                                                                T* __restrict__ dz_out, int64_t M, int C) {
+                                                                T* __restrict__ dz_out, int64_t M, int C,
+                                                                const T* __restrict__ y2 = nullptr,
+                                                                const float* __restrict__ mean2 = nullptr,
+                                                                const float* __restrict__ inv2 = nullptr,
+                                                                const float* __restrict__ coef2 = nullptr,
+                                                                T* __restrict__ dy2 = nullptr) {
   constexpr int E = V<T>::E;
   const int cpr = C / E;
   const int64_t total = M * cpr;
@@ -390,6 +443,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const T* __restr
     if constexpr (MK == 3) ov.x = reinterpret_cast<const uint8_t*>(out)[off / E];
     load_vec(y + off, yy);
     relu_mask<MK, T>(d, ov, yy, rs, rb, c0);
+    float y2f[DUAL ? E : 1];
+    if constexpr (DUAL) load_vec(y2 + off, y2f);
     if (dz_out) store_vec(dz_out + off, d);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -398,6 +453,15 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const T* __restr
       r[e] = coef[c] * (d[e] - coef[C + c] - xh * coef[2 * C + c]);
     }
     store_vec(dy + off, r);
+    if constexpr (DUAL) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int c = c0 + e;
+        const float xh = (y2f[e] - mean2[c]) * inv2[c];
+        r[e] = coef2[c] * (d[e] - coef2[C + c] - xh * coef2[2 * C + c]);
+      }
+      store_vec(dy2 + off, r);
+    }
   }
 }
 
@@ -544,7 +608,7 @@ int bn_bwd_impl(int mk, int32_t dtype, const void* dout, const void* out, const 
     auto k = mk == 1 ? bn_bwd_reduce2_kernel<TT, 1> : mk == 2 ? bn_bwd_reduce2_kernel<TT, 2>
            : mk == 3 ? bn_bwd_reduce2_kernel<TT, 3> : bn_bwd_reduce2_kernel<TT, 0>;
     k<<<grid, kThreads, 0, s>>>((const TT*)dout, (const TT*)out, relu_scale, relu_shift, (const TT*)y, mean, invstd,
-                                part, M, C, rpb);
+                                part, M, C, rpb, nullptr, nullptr, nullptr, nullptr);
   };
   if (dtype == POSE6D_DT_BF16) reduce((bf16*)nullptr);
   else reduce((float*)nullptr);
@@ -557,7 +621,8 @@ int bn_bwd_impl(int mk, int32_t dtype, const void* dout, const void* out, const 
     auto k = mk == 1 ? bn_bwd_apply_kernel<TT, 1> : mk == 2 ? bn_bwd_apply_kernel<TT, 2>
            : mk == 3 ? bn_bwd_apply_kernel<TT, 3> : bn_bwd_apply_kernel<TT, 0>;
     k<<<grid_for(M * C / V<TT>::E), kThreads, 0, s>>>((const TT*)dout, (const TT*)out, relu_scale, relu_shift,
-                                                      (const TT*)y, mean, invstd, coef, (TT*)dy, (TT*)dz_out, M, C);
+                                                      (const TT*)y, mean, invstd, coef, (TT*)dy, (TT*)dz_out, M, C, nullptr, nullptr,
+                                                      nullptr, nullptr, nullptr);
   };
   if (dtype == POSE6D_DT_BF16) apply((bf16*)nullptr);
   else apply((float*)nullptr);
@@ -565,6 +630,99 @@ int bn_bwd_impl(int mk, int32_t dtype, const void* dout, const void* out, const 
   return POSE6D_OK;
 }
 }  // namespace
+
+// The rest of a BatchNorm backward whose reduce pass ran in the data gradient that
+// produced dout (pose6d_conv2d_backward_chain_bn, `partial` [2][C][rows]): finalize +
+// apply, two launches; with partial2 / y2 / ... the dual branch BN too (grid.y = 2 in
+// the finalize, both dy in one apply).  relu: relu_mask bits (needed for the dual) or
+// relu_scale / relu_shift recomputed from y.  coef: 3 * C floats (6 * C dual).
+extern "C" int pose6d_bn_bwd_partials(int32_t dtype, const float* partial, int32_t rows, const void* dout,
+                                      const uint8_t* relu_mask, const float* relu_scale, const float* relu_shift,
+                                      const void* y, const float* mean, const float* invstd, const float* gamma,
+                                      float* dgamma, float* dbeta, void* dy, const float* partial2, const void* y2,
+                                      const float* mean2, const float* invstd2, const float* gamma2, float* dgamma2,
+                                      float* dbeta2, void* dy2, int32_t accumulate, float* coef, int64_t M, int32_t C,
+                                      void* stream) {
+  P6_CHECK_ARG(C % 8 == 0 && M > 0 && rows > 0 && partial && dout && y && dy && coef,
+               "pose6d_bn_bwd_partials: bad arguments");
+  P6_CHECK_ARG(relu_mask || (relu_scale && relu_shift), "pose6d_bn_bwd_partials: needs relu_mask or relu_scale/shift");
+  const bool dual = partial2 != nullptr;
+  P6_CHECK_ARG(!dual || (relu_mask && y2 && mean2 && invstd2 && gamma2 && dy2),
+               "pose6d_bn_bwd_partials: the second BatchNorm needs relu_mask, y2, mean2, invstd2, gamma2, dy2");
+  hipStream_t s = p6::stream_of(stream);
+  float* coef2 = coef + 3 * (int64_t)C;
+  const BwdFin b2{partial2, gamma2, invstd2, dgamma2, dbeta2, coef2};
+  bn_bwd_finalize_kernel<<<dim3(p6::ceil_div(C, kThreads / 64), dual ? 2 : 1), kThreads, 0, s>>>(
+      partial, rows, C, (double)M, gamma, invstd, dgamma, dbeta, accumulate, coef, b2);
+  P6_LAUNCH_CHECK();
+  auto apply = [&](auto* typed) {
+    using TT = std::remove_pointer_t<decltype(typed)>;
+    const dim3 grid = grid_for(M * C / V<TT>::E);
+    if (dual)
+      bn_bwd_apply_kernel<TT, 3, true><<<grid, kThreads, 0, s>>>(
+          (const TT*)dout, (const TT*)relu_mask, nullptr, nullptr, (const TT*)y, mean, invstd, coef, (TT*)dy, nullptr,
+          M, C, (const TT*)y2, mean2, invstd2, coef2, (TT*)dy2);
+    else if (relu_mask)
+      bn_bwd_apply_kernel<TT, 3><<<grid, kThreads, 0, s>>>((const TT*)dout, (const TT*)relu_mask, nullptr, nullptr,
+                                                           (const TT*)y, mean, invstd, coef, (TT*)dy, nullptr, M, C);
+    else
+      bn_bwd_apply_kernel<TT, 2><<<grid, kThreads, 0, s>>>((const TT*)dout, nullptr, relu_scale, relu_shift,
+                                                           (const TT*)y, mean, invstd, coef, (TT*)dy, nullptr, M, C);
+  };
+  if (dtype == POSE6D_DT_BF16) apply((bf16*)nullptr);
+  else apply((float*)nullptr);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+// Backward of a downsampling block's two BatchNorms at once: both are fed the same
+// dout * mask (the block output's gradient through its ReLU bits); bn 1 = y / mean /
+// invstd / gamma -> dy, bn 2 = y2 / ... -> dy2.  = pose6d_bn_bwd_mask(bn 1) then
+// pose6d_bn_bwd_mask(bn 2), bit for bit, in three launches instead of six, dout and the
+// mask read once per pass.  workspace: 2 * (pose6d_bn_bwd_workspace_rows(M) * 2 + 3) * C floats.
+extern "C" int pose6d_bn_bwd_mask_dual(int32_t dtype, const void* dout, const uint8_t* relu_mask, const void* y,
+                                       const float* mean, const float* invstd, const float* gamma, float* dgamma,
+                                       float* dbeta, void* dy, const void* y2, const float* mean2,
+                                       const float* invstd2, const float* gamma2, float* dgamma2, float* dbeta2,
+                                       void* dy2, int32_t accumulate, float* workspace, int64_t M, int32_t C,
+                                       void* stream) {
+  P6_CHECK_ARG(C % 8 == 0 && M > 0 && relu_mask && y && y2 && dy && dy2, "pose6d_bn_bwd_mask_dual: bad arguments");
+  hipStream_t s = p6::stream_of(stream);
+  const int rpb = rows_per_block(M);
+  const int nb = p6::ceil_div(M, rpb);
+  const int64_t one = ((int64_t)nb * 2 + 3) * C;
+  float* part = workspace;
+  float* coef = workspace + (int64_t)nb * 2 * C;
+  float* part2 = workspace + one;
+  float* coef2 = part2 + (int64_t)nb * 2 * C;
+  const int E = dtype == POSE6D_DT_BF16 ? 8 : 4;
+  const int cpr = C / E;
+  const int cl = cpr < 64 ? cpr : 64;
+  P6_CHECK_ARG(cpr % cl == 0 && kThreads % cl == 0, "pose6d_bn_bwd_mask_dual: C / vector width must be a power of two");
+  auto run = [&](auto* typed) {
+    using TT = std::remove_pointer_t<decltype(typed)>;
+    bn_bwd_reduce2_kernel<TT, 3, true><<<dim3(cpr / cl, nb), kThreads, 0, s>>>(
+        (const TT*)dout, (const TT*)relu_mask, nullptr, nullptr, (const TT*)y, mean, invstd, part, M, C, rpb,
+        (const TT*)y2, mean2, invstd2, part2);
+  };
+  if (dtype == POSE6D_DT_BF16) run((bf16*)nullptr);
+  else run((float*)nullptr);
+  P6_LAUNCH_CHECK();
+  const BwdFin b2{part2, gamma2, invstd2, dgamma2, dbeta2, coef2};
+  bn_bwd_finalize_kernel<<<dim3(p6::ceil_div(C, kThreads / 64), 2), kThreads, 0, s>>>(
+      part, nb, C, (double)M, gamma, invstd, dgamma, dbeta, accumulate, coef, b2);
+  P6_LAUNCH_CHECK();
+  auto apply = [&](auto* typed) {
+    using TT = std::remove_pointer_t<decltype(typed)>;
+    bn_bwd_apply_kernel<TT, 3, true><<<grid_for(M * C / V<TT>::E), kThreads, 0, s>>>(
+        (const TT*)dout, (const TT*)relu_mask, nullptr, nullptr, (const TT*)y, mean, invstd, coef, (TT*)dy, nullptr,
+        M, C, (const TT*)y2, mean2, invstd2, coef2, (TT*)dy2);
+  };
+  if (dtype == POSE6D_DT_BF16) apply((bf16*)nullptr);
+  else apply((float*)nullptr);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
 
 extern "C" int pose6d_channel_sum(int32_t dtype, const void* x, int64_t M, int32_t C, float* out, int32_t accumulate,
                                   void* stream) {

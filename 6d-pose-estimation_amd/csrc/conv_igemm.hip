@@ -62,7 +62,23 @@ struct Geom {
   const void* src2;
   const void* wts2;
   int Kpad2, SH2, SW2, stride2;
+  // data gradient that completes a BatchNorm's output gradient (pose6d_bn_reduce_t):
+  // the epilogue also sums that BN's dz = dX * relu and dz * xhat per channel over its
+  // tile into partial row bnr_rows-major [2][C][bnr_rows] (null bnr_part = off)
+  const void* bnr_y;
+  const float *bnr_mean, *bnr_inv, *bnr_rs, *bnr_rb;
+  const uint8_t* bnr_mask;
+  float* bnr_part;
+  const void* bnr_y2;
+  const float *bnr_mean2, *bnr_inv2;
+  float* bnr_part2;
+  int bnr_rows;
 };
+
+// LDS bytes the BN-reduce epilogue needs beyond the staged tile: per wave, per chunk
+// column, (sum dz, sum dz xhat, sum dz xhat2) x 16-byte chunk = 12 bytes per column,
+// + four per-channel constants
+constexpr int bnr_lds(int nw, int bn) { return 12 * nw * bn + 16 * bn; }
 
 // kDgradS2 launched in place (dres == dx) when a single parity class has taps
 // (1x1 stride 2): the other classes' pixels are already final, so the grid covers
@@ -113,7 +129,95 @@ __device__ __forceinline__ void load_f32s(const float* __restrict__ p, float (&f
 
 template <int NW> struct WaveGrid { static constexpr int WM = NW / 2, WN = 2, NT = 64 * NW; };
 
-template <typename T, int BM, int BN, int ACT = 0, int NW = 4, bool DUAL = false>
+// BatchNorm-backward partial sums of one tile (Geom::bnr_*): a thread's chunks share
+// one chunk column (E channels); lanes of a column fold by xor shuffles, waves through
+// LDS (`red`, past the staged tile), in a fixed order -- deterministic.  dz = dX as
+// stored (T) times the BN's ReLU: the stored bits (bnr_mask) or T(y * rs + rb) > 0
+// recomputed, exactly as pose6d_bn_bwd's reduce decides it.  The per-channel
+// constants sit in LDS (`cst` [4][BN]: mean, invstd, then rs, rb or mean2, invstd2),
+// read per 4-channel group where used: held in registers they cost the data-gradient
+// kernels two waves of occupancy.
+template <typename T, int BN, int NW, int IT>
+__device__ __forceinline__ void bnr_partials(const Geom& g, const uint4 (&ov)[IT], const bool (&okv)[IT],
+                                             const int64_t (&oidx)[IT], const uint4 (&yv)[IT],
+                                             const unsigned (&mb)[IT], float* red, const float* cst, int prow,
+                                             int n0) {
+  constexpr int E = 16 / (int)sizeof(T), CPR = BN * (int)sizeof(T) / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cl = (tid % CPR) * E;   // the chunk column's first channel within the tile
+  const bool dual = g.bnr_y2 != nullptr, mk3 = g.bnr_mask != nullptr;
+  float sd[E], sq[E], sq2[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) sd[e] = sq[e] = sq2[e] = 0.f;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    if (!okv[it]) continue;
+    T a[E], yy[E], y2[E];
+    __builtin_memcpy(a, &ov[it], 16);
+    __builtin_memcpy(yy, &yv[it], 16);
+    // the dual branch's y: loaded here, not prefetched (registers; still before the stores)
+    const uint4 y2v = dual ? *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(g.bnr_y2) + oidx[it])
+                           : uint4{0, 0, 0, 0};
+    __builtin_memcpy(y2, &y2v, 16);
+#pragma unroll
+    for (int e4 = 0; e4 < E; e4 += 4) {
+      const float4 mu = *reinterpret_cast<const float4*>(cst + cl + e4);
+      const float4 iv = *reinterpret_cast<const float4*>(cst + BN + cl + e4);
+      const float4 ca = *reinterpret_cast<const float4*>(cst + 2 * BN + cl + e4);
+      const float4 cb = *reinterpret_cast<const float4*>(cst + 3 * BN + cl + e4);
+      const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, i4[4] = {iv.x, iv.y, iv.z, iv.w};
+      const float a4[4] = {ca.x, ca.y, ca.z, ca.w}, b4[4] = {cb.x, cb.y, cb.z, cb.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = e4 + k;
+        const float y = p6::to_f(yy[e]);
+        const bool on = mk3 ? ((mb[it] >> e) & 1u) != 0u : p6::to_f(p6::from_f<T>(fmaf(y, a4[k], b4[k]))) > 0.f;
+        const float d = on ? p6::to_f(a[e]) : 0.f;
+        sd[e] += d;
+        sq[e] = fmaf(d, (y - m4[k]) * i4[k], sq[e]);
+        if (dual) sq2[e] = fmaf(d, (p6::to_f(y2[e]) - a4[k]) * b4[k], sq2[e]);
+      }
+    }
+    asm volatile("" ::: "memory");   // keep the constant reads per trip (not hoisted into registers)
+  }
+#pragma unroll
+  for (int o = CPR; o < 64; o <<= 1)
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      sd[e] += __shfl_xor(sd[e], o, 64);
+      sq[e] += __shfl_xor(sq[e], o, 64);
+      if (dual) sq2[e] += __shfl_xor(sq2[e], o, 64);
+    }
+  if (lane < CPR) {
+    float* r = red + (wave * CPR + lane) * 3 * E;
+#pragma unroll
+    for (int e = 0; e < E; ++e) { r[e] = sd[e]; r[E + e] = sq[e]; r[2 * E + e] = sq2[e]; }
+  }
+  __syncthreads();
+  if (tid < BN) {
+    const int cc = tid / E, e = tid - cc * E, c = n0 + tid;
+    float S = 0.f, Q = 0.f, Q2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const float* r = red + (w * CPR + cc) * 3 * E;
+      S += r[e];
+      Q += r[E + e];
+      Q2 += r[2 * E + e];
+    }
+    if (c < g.Ncols) {
+      const int64_t rows = g.bnr_rows;
+      g.bnr_part[(int64_t)c * rows + prow] = S;
+      g.bnr_part[((int64_t)g.Ncols + c) * rows + prow] = Q;
+      if (dual) {
+        g.bnr_part2[(int64_t)c * rows + prow] = S;
+        g.bnr_part2[((int64_t)g.Ncols + c) * rows + prow] = Q2;
+      }
+    }
+  }
+}
+
+// BNR: the BN-reduce epilogue (Geom::bnr_*) compiled in -- the data-gradient instances
+template <typename T, int BM, int BN, int ACT = 0, int NW = 4, bool DUAL = false, bool BNR = false>
 __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / (16 * (NW / 2))][BN / 32], char* smem, const Geom& g,
                                               const float* __restrict__ bias, const T* __restrict__ res,
                                               T* __restrict__ out, float* __restrict__ stats, int m0, int n0,
@@ -138,6 +242,25 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / (16 * (NW / 2))]
   int64_t oidx[IT];   // element offset of the trip's chunk in `out` (0 when out of range)
   uint4 rv[IT];
   unsigned mbv[IT];
+  constexpr int BI = BNR ? IT : 1;
+  uint4 byv[BI];       // BN reduce: the BN's input y chunks
+  unsigned bmv[BI];    // and its ReLU bits
+  const bool bnr = BNR && g.bnr_part != nullptr;
+  float bcst[4] = {0.f, 0.f, 0.f, 0.f};   // this thread's channel's constants (tid < BN)
+  if constexpr (BNR) {
+    if (bnr && tid < BN) {
+      const int c = n0 + tid < g.Ncols ? n0 + tid : 0;
+      bcst[0] = g.bnr_mean[c];
+      bcst[1] = g.bnr_inv[c];
+      if (g.bnr_y2) {
+        bcst[2] = g.bnr_mean2[c];
+        bcst[3] = g.bnr_inv2[c];
+      } else if (!g.bnr_mask) {
+        bcst[2] = g.bnr_rs[c];
+        bcst[3] = g.bnr_rb[c];
+      }
+    }
+  }
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     const int idx = tid + it * NT;
@@ -150,6 +273,14 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / (16 * (NW / 2))]
     if (res) {
       rv[it] = *reinterpret_cast<const uint4*>(res + oidx[it]);
       if (!act && g.res_mask) mbv[it] = g.res_mask[oidx[it] / E];
+    }
+    if constexpr (BNR) {
+      byv[it] = uint4{0, 0, 0, 0};
+      bmv[it] = 0u;
+      if (bnr) {
+        byv[it] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(g.bnr_y) + oidx[it]);
+        if (g.bnr_mask) bmv[it] = g.bnr_mask[oidx[it] / E];
+      }
     }
   }
   const int wm = wave >> 1, wn = wave & 1;
@@ -223,6 +354,13 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / (16 * (NW / 2))]
         if constexpr (DUAL)
           *reinterpret_cast<T*>(smem + (BM + lr) * CROW + lc * (int)sizeof(T)) = p6::from_f<T>(acc2[i][j][r]);
       }
+  float* bnr_cst = reinterpret_cast<float*>(smem + BM * CROW + 12 * NW * BN);
+  if constexpr (BNR) {
+    if (bnr && tid < BN) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) bnr_cst[k * BN + tid] = bcst[k];
+    }
+  }
   float asc[E], ash[E], arsc[E], arsh[E];
   // (issued after the accumulators are staged: their registers are free again)
   if (act) {
@@ -277,6 +415,13 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / (16 * (NW / 2))]
       __builtin_memcpy(&v, a, 16);
     }
     ov[it] = v;
+  }
+  if constexpr (BNR) {
+    if (bnr) {
+      const int prow = ((cls >= 0 && !g.s2one) ? cls : 0) * g.gm + m0 / BM;
+      bnr_partials<T, BN, NW, IT>(g, ov, okv, oidx, byv, bmv, reinterpret_cast<float*>(smem + BM * CROW), bnr_cst,
+                                  prow, n0);
+    }
   }
 #pragma unroll
   for (int it = 0; it < IT; ++it)
@@ -557,7 +702,7 @@ template <typename T> struct LK { static constexpr int CH = 16 / (int)sizeof(T),
 
 // one workgroup's work; `bid_in` = its index in this conv's sub-grid (the whole grid,
 // or the leading part of a fused backward launch), `smem` = the kernel's dynamic LDS
-template <typename T, int BM, int BN, int MODE, int S, bool ACT = false, int NW = 4>
+template <typename T, int BM, int BN, int MODE, int S, bool ACT = false, int NW = 4, bool BNR = false>
 __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* __restrict__ src,
                                               const T* __restrict__ wts, const float* __restrict__ bias,
                                               const T* __restrict__ res, T* __restrict__ out,
@@ -840,15 +985,17 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   if constexpr (DUAL)   // acc2 = the block GEMM, acc = the downsample branch
     conv_epilogue<T, BM, BN, 1, NW, true>(acc2, smem, g, bias, nullptr, out, nullptr, m0, n0, -1, acc);
   else
-    conv_epilogue<T, BM, BN, ACT ? 1 : 0, NW>(acc, smem, g, bias, res, out, stats, m0, n0, cls);
+    conv_epilogue<T, BM, BN, ACT ? 1 : 0, NW, false, BNR>(acc, smem, g, bias, res, out, stats, m0, n0, cls);
 }
 
-template <typename T, int BM, int BN, int MODE, int S, bool ACT, int NW>
+// BNR: data gradient with the BatchNorm-reduce epilogue (its own instance: the
+// forward 1x1 kernels, kGemm too, keep their register budget)
+template <typename T, int BM, int BN, int MODE, int S, bool ACT, int NW, bool BNR = false>
 __global__ __launch_bounds__(64 * NW) void conv_lds_kernel(const T* __restrict__ src, const T* __restrict__ wts,
                                                            const float* __restrict__ bias, const T* __restrict__ res,
                                                            T* __restrict__ out, float* __restrict__ stats, Geom g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv_lds_body<T, BM, BN, MODE, S, ACT, NW>(smem, blockIdx.x, src, wts, bias, res, out, stats, g);
+  conv_lds_body<T, BM, BN, MODE, S, ACT, NW, BNR>(smem, blockIdx.x, src, wts, bias, res, out, stats, g);
 }
 
 // Fused backward of one conv: workgroups [0, nd) compute the data gradient,
@@ -866,7 +1013,7 @@ __global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const bf16* __restri
   const int b = blockIdx.x;
   const int nw = gw.gm * gw.gn * gw.splits;
   if (b < nd_pad) {
-    if (b < nd) conv_lds_body<bf16, 64, 64, DMODE, DS>(smem, b, dy, wt, nullptr, dres, dx, nullptr, gd);
+    if (b < nd) conv_lds_body<bf16, 64, 64, DMODE, DS, false, 4, true>(smem, b, dy, wt, nullptr, dres, dx, nullptr, gd);
   } else if (b < nd_pad + nw) {
     // kGemm data gradient <=> pointwise conv: the weight gradient takes the pointwise body
     conv_wgrad_lds_body<64, 64, WS, DMODE == kGemm>(smem, b - nd_pad, x, dy, ws, gw);
@@ -905,13 +1052,21 @@ int launch_fast(const Geom& g0, const void* src, const void* w, const float* bia
   const int nk = fast_nk(MODE, g, LK<T>::KS);
   const int ring = (nk < S ? (nk > 0 ? nk : 1) : S) * (BM + BN) * 128;
   // kGemmDual stages both branches' tiles for its epilogue
-  const int epi = (MODE == kGemmDual ? 2 : 1) * BM * (BN * (int)sizeof(T) + 16);
+  const int epi = (MODE == kGemmDual ? 2 : 1) * BM * (BN * (int)sizeof(T) + 16) + (g.bnr_part ? bnr_lds(NW, BN) : 0);
   const int lds = ring > epi ? ring : epi;
   if (MODE == kDgradS2) s2_single_class(g, res, out);
   const int grid = g.gm * g.gn * (MODE == kDgradS2 ? s2_classes(g) : 1);
   if constexpr (MODE == kGemm || MODE == kFwd || MODE == kGemmDual) {
     if (g.act) {   // eval BN-act epilogue (pose6d_conv2d_fwd_act)
       conv_lds_kernel<T, BM, BN, MODE, S, true, NW><<<grid, 64 * NW, lds, s>>>(
+          (const T*)src, (const T*)w, bias, (const T*)res, (T*)out, stats, g);
+      P6_LAUNCH_CHECK();
+      return POSE6D_OK;
+    }
+  }
+  if constexpr (MODE == kGemm || MODE == kDgrad || MODE == kDgradS2) {
+    if (g.bnr_part) {   // data gradient + BatchNorm reduce
+      conv_lds_kernel<T, BM, BN, MODE, S, false, NW, true><<<grid, 64 * NW, lds, s>>>(
           (const T*)src, (const T*)w, bias, (const T*)res, (T*)out, stats, g);
       P6_LAUNCH_CHECK();
       return POSE6D_OK;
@@ -1247,9 +1402,41 @@ extern "C" int pose6d_conv2d_fwd_act_dual(int32_t dtype, const void* x, const vo
 }
 
 namespace {
+// BatchNorm-reduce partial rows of a data-gradient plan: one per output tile (x the four
+// parity classes of kDgradS2)
+// (0: a register-staged plan, which has no BN-reduce epilogue)
+int bnr_plan_rows(const Plan& p) {
+  if (!p.fast) return 0;
+  const int bm = (p.tile <= 1 || p.tile == 4 || p.tile == 5) ? 128 : 64;
+  return p6::ceil_div(p.g.M, bm) * (p.mode == kDgradS2 ? 4 : 1);
+}
+
+void set_bnr(Geom& g, const pose6d_bn_reduce_t* b) {
+  if (!b) return;
+  g.bnr_y = b->y; g.bnr_mean = b->mean; g.bnr_inv = b->invstd;
+  g.bnr_rs = b->relu_scale; g.bnr_rb = b->relu_shift; g.bnr_mask = b->relu_mask;
+  g.bnr_part = b->partial; g.bnr_rows = b->rows;
+  g.bnr_y2 = b->y2; g.bnr_mean2 = b->mean2; g.bnr_inv2 = b->invstd2; g.bnr_part2 = b->partial2;
+}
+
+int check_bnr(const pose6d_bn_reduce_t* b, const Plan& p, const void* dres, const void* dx) {
+  if (!b) return POSE6D_OK;
+  P6_CHECK_ARG(b->y && b->mean && b->invstd && b->partial, "pose6d_bn_reduce_t: null y / mean / invstd / partial");
+  P6_CHECK_ARG(b->relu_mask || (b->relu_scale && b->relu_shift),
+               "pose6d_bn_reduce_t: needs relu_mask or relu_scale + relu_shift");
+  P6_CHECK_ARG(!b->y2 || (b->relu_mask && b->mean2 && b->invstd2 && b->partial2),
+               "pose6d_bn_reduce_t: a second BatchNorm needs relu_mask, mean2, invstd2, partial2");
+  P6_CHECK_ARG(dres != dx, "pose6d_bn_reduce_t: the data gradient must be written whole (no in-place residual)");
+  P6_CHECK_ARG(p.fast, "pose6d_bn_reduce_t: this data gradient runs the register-staged kernel (no BN reduce)");
+  P6_CHECK_ARG(b->rows == bnr_plan_rows(p), "pose6d_bn_reduce_t: rows %d != %d (pose6d_conv2d_backward_bn_rows)",
+               b->rows, bnr_plan_rows(p));
+  return POSE6D_OK;
+}
+
 int dgrad_impl(int32_t dtype, const void* dy, const void* wt, const void* dres, const uint8_t* dres_mask, void* dx,
                int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
-               int32_t pad, int32_t Ho, int32_t Wo, void* stream, const pose6d_tuning_t* tn = nullptr) {
+               int32_t pad, int32_t Ho, int32_t Wo, void* stream, const pose6d_tuning_t* tn = nullptr,
+               const pose6d_bn_reduce_t* bnr = nullptr) {
   P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_dgrad: bad dtype %d", dtype);
   P6_CHECK_ARG(stride == 1 || stride == 2, "pose6d_conv2d_dgrad: stride must be 1 or 2");
   P6_CHECK_ARG(Cin % 8 == 0, "pose6d_conv2d_dgrad: Cin %% 8 != 0 (no data gradient for the stem)");
@@ -1259,6 +1446,11 @@ int dgrad_impl(int32_t dtype, const void* dy, const void* wt, const void* dres, 
   Geom g = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
   g.res_mask = dres_mask;
   P6_CHECK_ARG(g.log2SC >= 0 && Cout % bk == 0, "pose6d_conv2d_dgrad: Cout must be a power of two >= %d", bk);
+  if (bnr) {
+    const int rc = check_bnr(bnr, choose(dtype, mode, g, false, tn), dres, dx);
+    if (rc) return rc;
+    set_bnr(g, bnr);
+  }
   return run_conv(dtype, mode, g, dy, wt, nullptr, dres, dx, nullptr, p6::stream_of(stream), tn);
 }
 }  // namespace
@@ -1291,7 +1483,7 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
   const int nw = gw.gm * gw.gn * gw.splits;
   const int nk = fast_nk(DMODE, gd);
   const int ring_d = (nk < DS ? (nk > 0 ? nk : 1) : DS) * 128 * 128;
-  const int epi = 64 * (64 * 2 + 16);
+  const int epi = 64 * (64 * 2 + 16) + (gd.bnr_part ? bnr_lds(4, 64) : 0);
   const int ring_w = WS * 128 * 128;
   int lds = ring_d > epi ? ring_d : epi;
   lds = lds > ring_w ? lds : ring_w;
@@ -1326,7 +1518,8 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
                        int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
                        int32_t pad, int32_t Ho, int32_t Wo, int32_t phases, void* stream,
                        const ReduceJob* rj = nullptr, int32_t* deferred = nullptr,
-                       const uint8_t* dres_mask = nullptr, const pose6d_tuning_t* tn = nullptr) {
+                       const uint8_t* dres_mask = nullptr, const pose6d_tuning_t* tn = nullptr,
+                       const pose6d_bn_reduce_t* bnr = nullptr) {
   P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_backward: bad dtype %d", dtype);
   if (deferred) *deferred = 0;
   const ReduceJob none{};
@@ -1336,6 +1529,7 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
                                    rj->accumulate, p6::stream_of(stream));
   };
   P6_CHECK_ARG(phases >= 1 && phases <= 3, "pose6d_conv2d_backward_ex: phases must be 1, 2 or 3");
+  P6_CHECK_ARG(!bnr || (dx && phases == 3), "pose6d_conv2d_backward: a BatchNorm reduce needs the data gradient");
   if (dx == nullptr) {
     if (!(phases & 1)) return POSE6D_OK;
     const int rc = flush_prev();
@@ -1358,7 +1552,8 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
     if (!(phases & 1)) return POSE6D_OK;
     int rc = flush_prev();
     if (rc) return rc;
-    rc = dgrad_impl(dtype, dy, wt, dres, dres_mask, dx, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, stream, tn);
+    rc = dgrad_impl(dtype, dy, wt, dres, dres_mask, dx, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, stream, tn,
+                    bnr);
     if (rc) return rc;
     return pose6d_conv2d_wgrad_tuned(dtype, x, dy, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real, Cout,
                                      KH, KW, stride, pad, Ho, Wo, tn, stream);
@@ -1367,18 +1562,21 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
                "pose6d_conv2d_backward: workspace %lld bytes < %lld needed", (long long)ws_bytes,
                (long long)pw.splits * Cout * gw.Kpad * 4);
   hipStream_t s = p6::stream_of(stream);
-  int rc = POSE6D_OK;
+  int rc = check_bnr(bnr, pd, dres, dx);
+  if (rc) return rc;
+  Geom gd = pd.g;
+  set_bnr(gd, bnr);
   const ReduceJob& carried = rj ? *rj : none;
   if (phases & 1) {
     switch (pd.mode) {
       case kGemm:
-        rc = launch_bwd_mode<kGemm>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, carried, s);
+        rc = launch_bwd_mode<kGemm>(pd.stages, gd, gw, dy, wt, dres, dx, x, workspace, carried, s);
         break;
       case kDgradS2:
-        rc = launch_bwd_mode<kDgradS2>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, carried, s);
+        rc = launch_bwd_mode<kDgradS2>(pd.stages, gd, gw, dy, wt, dres, dx, x, workspace, carried, s);
         break;
       default:
-        rc = launch_bwd_mode<kDgrad>(pd.stages, pd.g, gw, dy, wt, dres, dx, x, workspace, carried, s);
+        rc = launch_bwd_mode<kDgrad>(pd.stages, gd, gw, dy, wt, dres, dx, x, workspace, carried, s);
         break;
     }
   }
@@ -1498,4 +1696,37 @@ extern "C" int pose6d_conv2d_backward_chain_masked(int32_t dtype, const void* x,
   }
   return conv_backward_impl(dtype, x, dy, wt, dres, dx, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real,
                             Cout, KH, KW, stride, pad, Ho, Wo, 3, stream, prev ? &r : nullptr, deferred, dres_mask);
+}
+
+// BatchNorm-reduce partial rows of this conv's data gradient (pose6d_bn_reduce_t::rows):
+// the plan pose6d_conv2d_backward_chain_bn will run, one row per output tile
+extern "C" int pose6d_conv2d_backward_bn_rows(int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t Cin,
+                                              int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad,
+                                              int32_t Ho, int32_t Wo) {
+  if (Cin % 8 != 0 || ilog2(Cin) < 3) return 0;
+  int mode;
+  const Geom gd0 = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
+  const Plan pd = choose(dtype, mode, gd0, true);
+  p6::WgradPlan pw;
+  p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
+  return bnr_plan_rows(bwd_fused(pd, pw, nullptr) ? pd : choose(dtype, mode, gd0, false));
+}
+
+extern "C" int pose6d_conv2d_backward_chain_bn(int32_t dtype, const void* x, const void* dy, const void* wt,
+                                               const void* dres, const uint8_t* dres_mask, void* dx, float* dw,
+                                               int32_t accumulate, float* workspace, int64_t ws_bytes, int32_t N,
+                                               int32_t H, int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout,
+                                               int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho,
+                                               int32_t Wo, const pose6d_wgrad_reduce_t* prev, int32_t* deferred,
+                                               const pose6d_bn_reduce_t* bn, void* stream) {
+  P6_CHECK_ARG(deferred != nullptr, "pose6d_conv2d_backward_chain_bn: deferred must point to an int32");
+  P6_CHECK_ARG(!dres_mask || dres, "pose6d_conv2d_backward_chain_bn: a mask needs dres");
+  ReduceJob r{};
+  if (prev) {
+    P6_CHECK_ARG(prev->ws != workspace, "pose6d_conv2d_backward_chain: prev slabs must live in another workspace");
+    r = make_job(*prev);
+  }
+  return conv_backward_impl(dtype, x, dy, wt, dres, dx, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real,
+                            Cout, KH, KW, stride, pad, Ho, Wo, 3, stream, prev ? &r : nullptr, deferred, dres_mask,
+                            nullptr, bn);
 }

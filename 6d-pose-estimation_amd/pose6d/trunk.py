@@ -33,6 +33,14 @@ class _WgradReduce(ctypes.Structure):
                                       "Ho", "Wo", "accumulate")]
 
 
+class _BnReduce(ctypes.Structure):
+    """pose6d_bn_reduce_t (include/pose6d.h): the BN whose backward sums a data
+    gradient's epilogue accumulates."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("y", "mean", "invstd", "relu_scale", "relu_shift", "relu_mask",
+                                                "partial", "y2", "mean2", "invstd2", "partial2")] + [
+        ("rows", ctypes.c_int32)]
+
+
 # pose6d_bn_fold_t (include/pose6d.h): eval-mode BN fold table entry
 _FOLD = np.dtype([("gamma", "<u8"), ("beta", "<u8"), ("rmean", "<u8"), ("rvar", "<u8"), ("scale", "<u8"),
                   ("shift", "<u8"), ("smean", "<u8"), ("sinv", "<u8"), ("eps", "<f4"), ("C", "<i4")])
@@ -226,8 +234,12 @@ class TrunkEngine:
                 op.mbits = (torch.empty(B * o.H * o.W * o.C // vec, device=device, dtype=torch.uint8)
                             if (op.relu and residual) else None)
                 op.dz = e(B, o.H, o.W, o.C) if (residual and op.mbits is None) else None
+                if op.res_conv is not None and op.mbits is not None:   # both BNs' partials at once
+                    ws_bn = max(ws_bn, 2 * (query("bn_bwd_workspace_rows", B * o.H * o.W) * 2 + 3) * o.C)
             elif isinstance(op, _PoolOp):
                 op.argmax = torch.empty(B, o.H, o.W, o.C, device=device, dtype=torch.uint8)
+        self._plan_bn_reduce(B, f32)
+        ws_bn = max(ws_bn, 6 * max(op.cout for op in self.convs))   # pose6d_bn_bwd_partials' coefficients
         self.ws_wgrad = f32(max(ws_w // 4, 1))
         self.ws_wgrad2 = f32(max(ws_w // 4, 1))   # ping-pong: a deferred slab reduce reads the other one
         self.ws_bn = f32(max(ws_bn, 1))
@@ -239,6 +251,43 @@ class TrunkEngine:
         self._desc_dev = None
         self._pack_key = None
         self._build_pack_table()
+
+    def _plan_bn_reduce(self, B, f32):
+        """A conv whose input is a BN + ReLU output that no other conv reads (each
+        bottleneck's conv2 / conv3, and conv1 of a block fed by an identity block) writes
+        that activation's whole gradient in one data-gradient launch: its epilogue also
+        sums the BN's backward partials (pose6d_conv2d_backward_chain_bn), so the BN
+        backward is finalize + apply (pose6d_bn_bwd_partials), without re-reading dout.
+        A downsampling block's input (read by conv1 and the downsample conv, the latter
+        adding into the former's gradient in place) keeps the three-pass backward."""
+        producer = {id(op.out): op for op in self.ops if isinstance(op, _ActOp)}
+        readers = {}
+        for op in self.convs:
+            readers.setdefault(id(op.src), []).append(op)
+        for op in self.ops:
+            if isinstance(op, _ActOp):
+                op.bnr = None
+            elif isinstance(op, _ConvOp):
+                op.bnr_desc = None
+        for op in self.convs:
+            p = producer.get(id(op.src))
+            if (p is None or p.pooled or not p.relu or not op.needs_dgrad or len(readers[id(op.src)]) != 1
+                    or p.res_act is not None and p.mbits is None or p.res_conv is not None and p.mbits is None):
+                continue
+            rows = query("conv2d_backward_bn_rows", self.dt, B, op.H, op.W, op.cin_pad, op.cout, op.k, op.k,
+                         op.stride, op.pad, op.Ho, op.Wo)
+            if rows <= 0:
+                continue
+            c, r = p.cop, p.res_conv
+            part = f32(2, c.cout, rows)
+            part2 = f32(2, r.cout, rows) if r is not None else None
+            ptr = lambda t: t.data_ptr() if t is not None else None
+            plain = p.mbits is None
+            op.bnr_desc = _BnReduce(ptr(c.out.t), ptr(c.mean), ptr(c.inv), ptr(c.scale) if plain else None,
+                                    ptr(c.shift) if plain else None, ptr(p.mbits), ptr(part),
+                                    ptr(r.out.t) if r else None, ptr(r.mean) if r else None,
+                                    ptr(r.inv) if r else None, ptr(part2), rows)
+            p.bnr = (part, part2, rows)
 
     def _eval_fold(self, st):
         """Eval scale/shift (+ saved mean / invstd) of every BN from its running
@@ -441,6 +490,26 @@ class TrunkEngine:
                 plain = op.relu and op.res_act is None and op.res_conv is None
                 out = op.out.t if (op.relu and not plain) else None
                 rs, rb = (c.scale, c.shift) if plain else (None, None)
+                r = op.res_conv
+                if op.bnr is not None and self.bwd_conv_bn_reduce:
+                    # the consumer's data gradient already summed this BN's partials
+                    part, part2, rows = op.bnr
+                    call("bn_bwd_partials", dt, part, rows, op.out.g, op.mbits, rs, rb, c.out.t, c.mean, c.inv,
+                         bn.weight.detach(), grad_of(bn.weight), grad_of(bn.bias), c.out.g, part2,
+                         r.out.t if r else None, r.mean if r else None, r.inv if r else None,
+                         r.bn.weight.detach() if r else None, grad_of(r.bn.weight) if r else None,
+                         grad_of(r.bn.bias) if r else None, r.out.g if r else None, acc, self.ws_bn, M, c.cout, st)
+                    if op.res_act is not None:
+                        op.res_act.pending = (op.out.g, op.mbits)
+                    continue
+                if r is not None and op.mbits is not None and self.bwd_dual_bn:
+                    # downsampling block: its last BN and the branch BN share dout * mask --
+                    # both backwards in one reduce / finalize / apply
+                    call("bn_bwd_mask_dual", dt, op.out.g, op.mbits, c.out.t, c.mean, c.inv, bn.weight.detach(),
+                         grad_of(bn.weight), grad_of(bn.bias), c.out.g, r.out.t, r.mean, r.inv,
+                         r.bn.weight.detach(), grad_of(r.bn.weight), grad_of(r.bn.bias), r.out.g, acc, self.ws_bn,
+                         M, c.cout, st)
+                    continue
                 if op.mbits is not None:
                     call("bn_bwd_mask", dt, op.out.g, op.mbits, c.out.t, c.mean, c.inv, bn.weight.detach(),
                          grad_of(bn.weight), grad_of(bn.bias), acc, c.out.g, op.dz, self.ws_bn, M, c.cout, st)
@@ -490,7 +559,10 @@ class TrunkEngine:
                 job = _WgradReduce(ws.data_ptr(), dw.data_ptr(), dt, B, op.H, op.W, op.cin_pad, op.cin, op.cout,
                                    op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, acc)
                 prev = ctypes.addressof(pending) if pending is not None else None
-                if dmask is not None:
+                if op.bnr_desc is not None and self.bwd_conv_bn_reduce:
+                    call("conv2d_backward_chain_bn", dt, op.src.t, dy, op.wt, dres, dmask, *args[5:], prev,
+                         ctypes.addressof(deferred), ctypes.addressof(op.bnr_desc), st)
+                elif dmask is not None:
                     call("conv2d_backward_chain_masked", dt, op.src.t, dy, op.wt, dres, dmask, *args[5:], prev,
                          ctypes.addressof(deferred), st)
                 else:
@@ -530,6 +602,12 @@ class TrunkEngine:
     eval_fuse = True
     eval_dual = True
     eval_dual_rows = 16384
+    # training backward: a downsampling block's two BatchNorm backwards in one set of
+    # launches (bit-identical to two pose6d_bn_bwd_mask calls; attribute for the tests)
+    bwd_dual_bn = True
+    # training backward: a BN + ReLU whose output gradient one data-gradient launch
+    # completes gets its reduce pass from that launch's epilogue (attribute for the tests)
+    bwd_conv_bn_reduce = True
 
     def set_dtype(self, dtype):
         self.dtype_req = dtype

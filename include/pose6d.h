@@ -311,6 +311,40 @@ int pose6d_conv2d_backward_chain_masked(int32_t dtype, const void *x, const void
                                         int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH,
                                         int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
                                         const pose6d_wgrad_reduce_t *prev, int32_t *deferred, void *stream);
+
+/* A BatchNorm backward's reduce pass folded into the data gradient that completes
+ * its output gradient (the BN + ReLU producing this conv's input): while storing dX
+ * (+ dres * mask), the epilogue also sums, per channel over each output tile,
+ * dz = dX * relu and dz * (y - mean) * invstd into partial[2][C][rows] -- what
+ * pose6d_bn_bwd's first launch computes from dX re-read.  relu = the stored bits
+ * (relu_mask, pose6d_bn_act_fwd_mask) or T(y * relu_scale + relu_shift) > 0;
+ * y2 / mean2 / invstd2 / partial2: a second BN fed the same dz (a downsampling
+ * block's branch BN; needs relu_mask).  rows = pose6d_conv2d_backward_bn_rows.
+ * pose6d_bn_bwd_partials then finishes the backward (finalize + apply). */
+typedef struct {
+  const void *y;
+  const float *mean, *invstd;
+  const float *relu_scale, *relu_shift;
+  const uint8_t *relu_mask;
+  float *partial;
+  const void *y2;
+  const float *mean2, *invstd2;
+  float *partial2;
+  int32_t rows;
+} pose6d_bn_reduce_t;
+
+int pose6d_conv2d_backward_bn_rows(int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout,
+                                   int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo);
+
+/* pose6d_conv2d_backward_chain (dres_mask as in _masked, or NULL) whose data gradient
+ * also produces the BatchNorm-reduce partials `bn` describes (NULL = none); dX must be
+ * written whole (dres != dx). */
+int pose6d_conv2d_backward_chain_bn(int32_t dtype, const void *x, const void *dy, const void *wt, const void *dres,
+                                    const uint8_t *dres_mask, void *dx, float *dw, int32_t accumulate,
+                                    float *workspace, int64_t ws_bytes, int32_t N, int32_t H, int32_t W, int32_t Cin,
+                                    int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
+                                    int32_t pad, int32_t Ho, int32_t Wo, const pose6d_wgrad_reduce_t *prev,
+                                    int32_t *deferred, const pose6d_bn_reduce_t *bn, void *stream);
 /* (1 << 16) | (data-gradient mode << 4) | ring stages when pose6d_conv2d_backward
  * runs ONE fused conv_bwd_kernel<mode, stages, 3> launch (+ the reduce), else 0 */
 int pose6d_bwd_variant(int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH,
@@ -360,6 +394,29 @@ int pose6d_bn_bwd_workspace_rows(int64_t M);
 int pose6d_bn_bwd_mask(int32_t dtype, const void *dout, const uint8_t *relu_mask, const void *y, const float *mean,
                        const float *invstd, const float *gamma, float *dgamma, float *dbeta, int32_t accumulate,
                        void *dy, void *dz_out, float *workspace, int64_t M, int32_t C, void *stream);
+/* The rest of a BatchNorm backward whose reduce pass ran in the data gradient that
+ * produced dout (pose6d_conv2d_backward_chain_bn's `partial`, [2][C][rows]): the
+ * finalize (dgamma, dbeta written or accumulated) and the apply (dy), two launches.
+ * relu = relu_mask bits or T(y * relu_scale + relu_shift) > 0.  partial2 / y2 / mean2 /
+ * invstd2 / gamma2 / dgamma2 / dbeta2 / dy2 (or NULL partial2): a second BN fed the
+ * same dout * mask (needs relu_mask).  coef: 3 * C floats (6 * C with the second BN). */
+int pose6d_bn_bwd_partials(int32_t dtype, const float *partial, int32_t rows, const void *dout,
+                           const uint8_t *relu_mask, const float *relu_scale, const float *relu_shift, const void *y,
+                           const float *mean, const float *invstd, const float *gamma, float *dgamma, float *dbeta,
+                           void *dy, const float *partial2, const void *y2, const float *mean2, const float *invstd2,
+                           const float *gamma2, float *dgamma2, float *dbeta2, void *dy2, int32_t accumulate,
+                           float *coef, int64_t M, int32_t C, void *stream);
+
+/* The backward of a downsampling block's two BatchNorms (the block's last BN and its
+ * downsample branch's BN, both fed dout * relu_mask): pose6d_bn_bwd_mask for (y, mean,
+ * invstd, gamma -> dgamma, dbeta, dy) and for (y2, ... -> dy2), bit for bit, in three
+ * launches (one reduce, one finalize, one apply: dout and the mask read once per pass).
+ * workspace: 2 * (pose6d_bn_bwd_workspace_rows(M) * 2 + 3) * C floats. */
+int pose6d_bn_bwd_mask_dual(int32_t dtype, const void *dout, const uint8_t *relu_mask, const void *y,
+                            const float *mean, const float *invstd, const float *gamma, float *dgamma, float *dbeta,
+                            void *dy, const void *y2, const float *mean2, const float *invstd2, const float *gamma2,
+                            float *dgamma2, float *dbeta2, void *dy2, int32_t accumulate, float *workspace, int64_t M,
+                            int32_t C, void *stream);
 int pose6d_bn_bwd(int32_t dtype, const void *dout, const void *out, const float *relu_scale,
                   const float *relu_shift, const void *y, const float *mean, const float *invstd, const float *gamma,
                   float *dgamma, float *dbeta, int32_t accumulate, void *dy, void *dz_out, float *workspace,
