@@ -157,8 +157,8 @@ def conv_flops(name, args, sym):
         N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo = args[6:17] if name == "conv2d_fwd" else args[5:16]
         cin = 3 if Cin == 4 else Cin   # the padded stem input (RGB padded to 4 channels)
         return 2.0 * N * Ho * Wo * Cout * KH * KW * cin
-    if name in ("conv2d_backward_chain", "conv2d_backward_chain_masked"):
-        i0 = 11 if name == "conv2d_backward_chain_masked" else 10
+    if name in _BWD_N_INDEX:
+        i0 = _BWD_N_INDEX[name]
         N, H, W, Cin, Cin_real, Cout, KH, KW, stride, pad, Ho, Wo = args[i0:i0 + 12]
         one = 2.0 * N * Ho * Wo * Cout * KH * KW * Cin_real
         if sym.startswith("conv_bwd_kernel"):
@@ -172,9 +172,55 @@ def conv_flops(name, args, sym):
     return None
 
 
+def conv_bytes(name, args, sym):
+    """Algorithmic HBM bytes of the kernel `sym` launched by pose6d_<name>(*args): every
+    operand read once and every result written once (activations in the call's dtype,
+    weights as packed, fp32 dW, the residual gradient and its ReLU bits where the call
+    carries them); None where conv_flops is None, 0 for the slab reduce (its bytes ride
+    in the fused launch that carries it)."""
+    if "reduce" in sym and "wgrad" in sym:
+        return 0.0
+    if name in ("conv2d_fwd", "conv2d_fwd_act"):
+        dt = args[0]
+        N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo = args[6:17] if name == "conv2d_fwd" else args[5:16]
+        e = 4 if dt == 0 else 2
+        b = e * (N * H * W * Cin + Cout * KH * KW * Cin + N * Ho * Wo * Cout)
+        if name == "conv2d_fwd_act" and args[18] is not None:   # residual added in the epilogue
+            b += e * N * Ho * Wo * Cout
+        return float(b)
+    if name in _BWD_N_INDEX:
+        i0 = _BWD_N_INDEX[name]
+        dt = args[0]
+        e = 4 if dt == 0 else 2
+        N, H, W, Cin, Cin_real, Cout, KH, KW, stride, pad, Ho, Wo = args[i0:i0 + 12]
+        x = N * H * W * Cin * e
+        dy = N * Ho * Wo * Cout * e
+        w = Cout * KH * KW * Cin * e
+        dw = Cout * KH * KW * Cin_real * 4
+        dres = args[4] is not None   # in place (dres == dx) it is still read
+        dgrad = (x + dy + w + (x if dres else 0) + (N * H * W * Cin // 8 if name != "conv2d_backward_chain" and
+                                                     args[5] is not None else 0))
+        wgrad = x + dy + dw
+        if sym.startswith("conv_bwd_kernel"):
+            return float(dgrad + wgrad - dy)   # dY read once by the fused launch
+        if args[i0 - 5] is None:
+            return float(wgrad) if "wgrad" in sym else 0.0
+        return float(wgrad if "wgrad" in sym else dgrad)
+    if name == "conv2d_fwd_act_dual":
+        dt = args[0]
+        e = 4 if dt == 0 else 2
+        N, Ho, Wo, Cin, Cout, Hd, Wd, Cind = args[6:14]
+        return float(e * (N * Ho * Wo * (Cin + Cout + Cind) + Cout * (Cin + Cind)))   # xd read at the sampled pixels
+    return None
+
+
+# index of N in the argument list of the backward entry points
+_BWD_N_INDEX = {"conv2d_backward_chain": 10, "conv2d_backward_chain_masked": 11, "conv2d_backward_chain_bn": 11}
+
+
 def conv_geom(name, args):
     """'N HxW Cin->Cout kKsS' of a conv call (None otherwise), for per-launch listings."""
-    idx = {"conv2d_fwd": 6, "conv2d_fwd_act": 5, "conv2d_backward_chain": 10, "conv2d_backward_chain_masked": 11}
+    idx = {"conv2d_fwd": 6, "conv2d_fwd_act": 5, **_BWD_N_INDEX}
     if name not in idx:
         return None
     i = idx[name]
@@ -239,7 +285,8 @@ class StepTimer:
                 sym = short_name(nm) if nm else "?"
             name, args = owner[i] if owner[i] else (None, None)
             fl = conv_flops(name, args, sym) if (sym and name) else None
-            self.records.append({"node": i, "type": t.value, "kernel": sym, "call": name, "flops": fl,
+            nb = conv_bytes(name, args, sym) if (sym and name) else None
+            self.records.append({"node": i, "type": t.value, "kernel": sym, "call": name, "flops": fl, "bytes": nb,
                                  "geom": conv_geom(name, args) if name else None})
             # splice: deps(node) -> event_i -> node
             ev = ctypes.c_void_p()
@@ -299,7 +346,7 @@ def by_symbol(records):
     agg = collections.OrderedDict()
     for r in records:
         a = agg.setdefault(r["kernel"], {"launches": 0, "time_us": 0.0, "time_raw_us": 0.0, "flops": 0.0,
-                                         "flops_known": True})
+                                         "flops_known": True, "bytes": 0.0})
         a["launches"] += 1
         a["time_us"] += r["us"]
         a["time_raw_us"] += r.get("us_raw", r["us"])
@@ -307,4 +354,5 @@ def by_symbol(records):
             a["flops_known"] = False
         else:
             a["flops"] += r["flops"]
+            a["bytes"] += r.get("bytes") or 0.0
     return collections.OrderedDict(sorted(agg.items(), key=lambda kv: -kv[1]["time_us"]))

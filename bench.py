@@ -289,9 +289,25 @@ def kernel_profile(tr, data, step_ms, peak_tflops=None, with_forward=True, reps=
     # SQ_VALU_MFMA_BUSY_CYCLES summed over the chip's 1024 SIMDs; busy fraction at 2.4 GHz
     mfma_busy = (round(pmc["mfma_busy_cycles_per_launch"] / (avg_t * 2.4e9 * 1024), 4)
                  if pmc and "mfma_busy_cycles_per_launch" in pmc else None)
+    # the roof that binds this kernel: the larger of its MFMA time floor (algorithmic
+    # flops / dense peak) and its HBM time floor (algorithmic bytes / 8 TB/s)
+    nbytes = a["bytes"] / a["launches"]
+    t_mfma = a["flops"] / a["launches"] / (peak_tflops * 1e12)
+    t_hbm = nbytes / (PEAK_HBM_GBS * 1e9)
+    hbm_gbs = nbytes / avg_t / 1e9
+    if t_hbm > t_mfma:
+        roof = {"bound": "hbm", "achieved": round(hbm_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(hbm_gbs / PEAK_HBM_GBS, 4)}
+    else:
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak_tflops, "unit": "TFLOP/s",
+                "frac": round(achieved / peak_tflops, 4)}
     out = {
-        "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak_tflops, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak_tflops, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+        "roofline": {**roof, "traffic": traffic, "traffic_unit": "bytes/launch",
+                     "mfma": {"achieved": round(achieved, 2), "peak": peak_tflops, "unit": "TFLOP/s",
+                              "frac": round(achieved / peak_tflops, 4), "floor_us": round(t_mfma * 1e6, 2)},
+                     "hbm": {"achieved": round(hbm_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": round(hbm_gbs / PEAK_HBM_GBS, 4), "floor_us": round(t_hbm * 1e6, 2)},
+                     "algorithmic_bytes_per_launch": round(nbytes),
                      "traffic_source": tsrc, "mfma_busy": mfma_busy,
                      "kernel": sym, "launches_per_step": a["launches"],
                      "avg_launch_us": round(avg_t * 1e6, 2),
@@ -301,7 +317,8 @@ def kernel_profile(tr, data, step_ms, peak_tflops=None, with_forward=True, reps=
                                f"overhead ({timer.overhead_us:.2f} us/node = (instrumented - plain step) / nodes)",
                      "avg_launch_us_raw_events": round(a["time_raw_us"] / a["launches"], 2),
                      "per_launch": [[r["geom"], round(r["us"], 2),
-                                     round(r["flops"] / (r["us"] * 1e-6) / 1e12, 1) if r["us"] > 0 else None]
+                                     round(r["flops"] / (r["us"] * 1e-6) / 1e12, 1) if r["us"] > 0 else None,
+                                     round((r.get("bytes") or 0) / (r["us"] * 1e-6) / 1e9, 1) if r["us"] > 0 else None]
                                     for r in recs if r["kernel"] == sym]},
         "breakdown": {"kernels_per_step": len(recs), "gpu_busy_ms_per_step": round(busy_ms, 3),
                       "instrumented_step_ms": round(inst_ms, 3), "step_ms": round(step_ms, 3),
