@@ -216,12 +216,84 @@ __device__ __forceinline__ void bnr_partials(const Geom& g, const uint4 (&ov)[IT
   }
 }
 
-// BNR: the BN-reduce epilogue (Geom::bnr_*) compiled in -- the data-gradient instances
+// What the epilogue's store loop reads from global memory besides the tile: the
+// residual chunks and their mask bytes, and for the BN-reduce epilogue the BN's input
+// y chunks, its ReLU bits and per-channel constants (epi_prefetch).  Kept apart from
+// conv_epilogue so that a workgroup with one or two K-steps can issue these loads
+// right behind its operand DMA (one memory round trip instead of two per workgroup:
+// the 1x1 data gradients with K = Cout = 64 / 128 are a DMA wait, 8 MFMAs and this
+// epilogue).
+template <typename T, int BM, int BN, int NW, bool BNR>
+struct EpiPre {
+  static constexpr int CPR = BN * (int)sizeof(T) / 16;                 // 16-B chunks per tile row
+  static constexpr int IT = (BM * CPR + 64 * NW - 1) / (64 * NW);      // store-loop trips per thread
+  static constexpr int BI = BNR ? IT : 1;
+  bool okv[IT];
+  int64_t oidx[IT];    // element offset of the trip's chunk in `out` (0 when out of range)
+  uint4 rv[IT];
+  unsigned mbv[IT];
+  uint4 byv[BI];       // BN reduce: the BN's input y chunks
+  unsigned bmv[BI];    // and its ReLU bits
+  float bcst[4];       // this thread's channel's BN-reduce constants (tid < BN)
+};
+
+template <typename T, int BM, int BN, int ACT, int NW, bool BNR>
+__device__ __forceinline__ void epi_prefetch(EpiPre<T, BM, BN, NW, BNR>& p, const Geom& g,
+                                             const T* __restrict__ res, int m0, int n0, int cls) {
+  using P = EpiPre<T, BM, BN, NW, BNR>;
+  constexpr int NT = WaveGrid<NW>::NT, CPR = P::CPR, IT = P::IT;
+  constexpr int E = 16 / (int)sizeof(T);
+  constexpr bool act = ACT == 1;
+  const int tid = threadIdx.x;
+  const bool bnr = BNR && g.bnr_part != nullptr;
+  for (int k = 0; k < 4; ++k) p.bcst[k] = 0.f;
+  if constexpr (BNR) {
+    if (bnr && tid < BN) {
+      const int c = n0 + tid < g.Ncols ? n0 + tid : 0;
+      p.bcst[0] = g.bnr_mean[c];
+      p.bcst[1] = g.bnr_inv[c];
+      if (g.bnr_y2) {
+        p.bcst[2] = g.bnr_mean2[c];
+        p.bcst[3] = g.bnr_inv2[c];
+      } else if (!g.bnr_mask) {
+        p.bcst[2] = g.bnr_rs[c];
+        p.bcst[3] = g.bnr_rb[c];
+      }
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int idx = tid + it * NT;
+    const int lr = idx / CPR, cc = idx - lr * CPR;
+    const int m = m0 + lr, c = n0 + cc * E;
+    p.okv[it] = idx < BM * CPR && m < g.M && c < g.Ncols;
+    p.oidx[it] = p.okv[it] ? out_row(g, cls, m) * g.Ncols + c : 0;
+    p.rv[it] = uint4{0, 0, 0, 0};
+    p.mbv[it] = 0xFFu;
+    if (res) {
+      p.rv[it] = *reinterpret_cast<const uint4*>(res + p.oidx[it]);
+      if (!act && g.res_mask) p.mbv[it] = g.res_mask[p.oidx[it] / E];
+    }
+    if constexpr (BNR) {
+      p.byv[it] = uint4{0, 0, 0, 0};
+      p.bmv[it] = 0u;
+      if (bnr) {
+        p.byv[it] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(g.bnr_y) + p.oidx[it]);
+        if (g.bnr_mask) p.bmv[it] = g.bnr_mask[p.oidx[it] / E];
+      }
+    }
+  }
+}
+
+// BNR: the BN-reduce epilogue (Geom::bnr_*) compiled in -- the data-gradient instances.
+// `pre`: the store loop's global operands, already fetched (epi_prefetch) when
+// `pre_done`, else fetched here first.
 template <typename T, int BM, int BN, int ACT = 0, int NW = 4, bool DUAL = false, bool BNR = false>
 __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / (16 * (NW / 2))][BN / 32], char* smem, const Geom& g,
                                               const float* __restrict__ bias, const T* __restrict__ res,
                                               T* __restrict__ out, float* __restrict__ stats, int m0, int n0,
-                                              int cls = -1, const f32x4 (*acc2)[BN / 32] = nullptr) {
+                                              int cls, const f32x4 (*acc2)[BN / 32],
+                                              EpiPre<T, BM, BN, NW, BNR>& pre, bool pre_done) {
   constexpr int WM = WaveGrid<NW>::WM, NT = WaveGrid<NW>::NT;
   constexpr int TM = BM / (16 * WM), TN = BN / 32;
   static_assert(TM % 2 == 0, "BatchNorm partials cover 32-row blocks of one wave");
@@ -238,51 +310,15 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / (16 * (NW / 2))]
   // issued after a store can only be waited for with vmcnt(0), which waits for the
   // store's acknowledgement too -- a full memory round trip per trip of the store loop
   // (measured: the eval 1x1 convs took 1.2-2.2x their plain-store time that way).
-  bool okv[IT];
-  int64_t oidx[IT];   // element offset of the trip's chunk in `out` (0 when out of range)
-  uint4 rv[IT];
-  unsigned mbv[IT];
-  constexpr int BI = BNR ? IT : 1;
-  uint4 byv[BI];       // BN reduce: the BN's input y chunks
-  unsigned bmv[BI];    // and its ReLU bits
+  if (!pre_done) epi_prefetch<T, BM, BN, ACT, NW, BNR>(pre, g, res, m0, n0, cls);
+  const bool (&okv)[IT] = pre.okv;
+  const int64_t (&oidx)[IT] = pre.oidx;
+  const uint4 (&rv)[IT] = pre.rv;
+  const unsigned (&mbv)[IT] = pre.mbv;
+  const auto& byv = pre.byv;
+  const auto& bmv = pre.bmv;
+  const float (&bcst)[4] = pre.bcst;
   const bool bnr = BNR && g.bnr_part != nullptr;
-  float bcst[4] = {0.f, 0.f, 0.f, 0.f};   // this thread's channel's constants (tid < BN)
-  if constexpr (BNR) {
-    if (bnr && tid < BN) {
-      const int c = n0 + tid < g.Ncols ? n0 + tid : 0;
-      bcst[0] = g.bnr_mean[c];
-      bcst[1] = g.bnr_inv[c];
-      if (g.bnr_y2) {
-        bcst[2] = g.bnr_mean2[c];
-        bcst[3] = g.bnr_inv2[c];
-      } else if (!g.bnr_mask) {
-        bcst[2] = g.bnr_rs[c];
-        bcst[3] = g.bnr_rb[c];
-      }
-    }
-  }
-#pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int idx = tid + it * NT;
-    const int lr = idx / CPR, cc = idx - lr * CPR;
-    const int m = m0 + lr, c = n0 + cc * E;
-    okv[it] = idx < BM * CPR && m < g.M && c < g.Ncols;
-    oidx[it] = okv[it] ? out_row(g, cls, m) * g.Ncols + c : 0;
-    rv[it] = uint4{0, 0, 0, 0};
-    mbv[it] = 0xFFu;
-    if (res) {
-      rv[it] = *reinterpret_cast<const uint4*>(res + oidx[it]);
-      if (!act && g.res_mask) mbv[it] = g.res_mask[oidx[it] / E];
-    }
-    if constexpr (BNR) {
-      byv[it] = uint4{0, 0, 0, 0};
-      bmv[it] = 0u;
-      if (bnr) {
-        byv[it] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(g.bnr_y) + oidx[it]);
-        if (g.bnr_mask) bmv[it] = g.bnr_mask[oidx[it] / E];
-      }
-    }
-  }
   const int wm = wave >> 1, wn = wave & 1;
   const int fr = lane & 15, fc = lane >> 4;
   const int row_base = m0 + wm * (BM / WM);
@@ -606,7 +642,8 @@ __global__ __launch_bounds__(kThreads) void conv_igemm_kernel(const T* __restric
     __syncthreads();
   }
 
-  conv_epilogue<T, BM, BN, ACT ? 1 : 0>(acc, smem, g, bias, res, out, stats, m0, n0);
+  EpiPre<T, BM, BN, 4, false> pre;
+  conv_epilogue<T, BM, BN, ACT ? 1 : 0>(acc, smem, g, bias, res, out, stats, m0, n0, -1, nullptr, pre, false);
 }
 
 // ============================================================================
@@ -702,7 +739,14 @@ template <typename T> struct LK { static constexpr int CH = 16 / (int)sizeof(T),
 
 // one workgroup's work; `bid_in` = its index in this conv's sub-grid (the whole grid,
 // or the leading part of a fused backward launch), `smem` = the kernel's dynamic LDS
-template <typename T, int BM, int BN, int MODE, int S, bool ACT = false, int NW = 4, bool BNR = false>
+// PRE: a workgroup with at most two K-steps fetches its epilogue's global operands
+// (epi_prefetch) right after issuing its operand DMA (build-time switch for A/B
+// timing: -DPOSE6D_EPI_PRE=0 builds the fetch-after-the-loop form)
+#ifndef POSE6D_EPI_PRE
+#define POSE6D_EPI_PRE 1
+#endif
+template <typename T, int BM, int BN, int MODE, int S, bool ACT = false, int NW = 4, bool BNR = false,
+          bool PRE = false>
 __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* __restrict__ src,
                                               const T* __restrict__ wts, const float* __restrict__ bias,
                                               const T* __restrict__ res, T* __restrict__ out,
@@ -957,6 +1001,12 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
 
   // prologue: stages 0 .. S-2 in flight; step kt refills the buffer step kt-1 read
   for (int s = 0; s < S - 1 && s < nk; ++s) issue(s, s);
+  // early epilogue fetch (PRE): younger than the prologue DMA, so the loop's counted
+  // waits (which count DMA only) over-wait it on the first step -- correct, and with
+  // one or two K-steps the two sets of loads are in flight together
+  EpiPre<T, BM, BN, NW, BNR> pre;
+  const bool early = POSE6D_EPI_PRE && PRE && !DUAL && nk <= 2;
+  if (early) epi_prefetch<T, BM, BN, ACT ? 1 : 0, NW, BNR>(pre, g, res, m0, n0, cls);
   int cur = 0, wbuf = S - 1;
   for (int kt = 0; kt < nk; ++kt) {
     const int left = nk - 1 - kt;
@@ -983,9 +1033,10 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   }
   asm volatile("s_barrier" ::: "memory");   // every wave done reading the ring before the epilogue reuses it
   if constexpr (DUAL)   // acc2 = the block GEMM, acc = the downsample branch
-    conv_epilogue<T, BM, BN, 1, NW, true>(acc2, smem, g, bias, nullptr, out, nullptr, m0, n0, -1, acc);
+    conv_epilogue<T, BM, BN, 1, NW, true>(acc2, smem, g, bias, nullptr, out, nullptr, m0, n0, -1, acc, pre, false);
   else
-    conv_epilogue<T, BM, BN, ACT ? 1 : 0, NW, false, BNR>(acc, smem, g, bias, res, out, stats, m0, n0, cls);
+    conv_epilogue<T, BM, BN, ACT ? 1 : 0, NW, false, BNR>(acc, smem, g, bias, res, out, stats, m0, n0, cls, nullptr,
+                                                          pre, early);
 }
 
 // BNR: data gradient with the BatchNorm-reduce epilogue (its own instance: the
@@ -1013,7 +1064,8 @@ __global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const bf16* __restri
   const int b = blockIdx.x;
   const int nw = gw.gm * gw.gn * gw.splits;
   if (b < nd_pad) {
-    if (b < nd) conv_lds_body<bf16, 64, 64, DMODE, DS, false, 4, true>(smem, b, dy, wt, nullptr, dres, dx, nullptr, gd);
+    if (b < nd)
+      conv_lds_body<bf16, 64, 64, DMODE, DS, false, 4, true, true>(smem, b, dy, wt, nullptr, dres, dx, nullptr, gd);
   } else if (b < nd_pad + nw) {
     // kGemm data gradient <=> pointwise conv: the weight gradient takes the pointwise body
     conv_wgrad_lds_body<64, 64, WS, DMODE == kGemm>(smem, b - nd_pad, x, dy, ws, gw);

@@ -201,6 +201,17 @@ def conv_bytes(name, args, sym):
         dgrad = (x + dy + w + (x if dres else 0) + (N * H * W * Cin // 8 if name != "conv2d_backward_chain" and
                                                      args[5] is not None else 0))
         wgrad = x + dy + dw
+        bn = args[-2] if name == "conv2d_backward_chain_bn" else None
+        if bn:
+            # the BN-reduce epilogue reads the BN's input y (and a second BN's y2) and
+            # its ReLU bits: pose6d_bn_reduce_t {y, mean, invstd, rs, rb, relu_mask,
+            # partial, y2, ...}, 8-byte pointers
+            ptr = ctypes.c_void_p.from_address
+            dgrad += x
+            if ptr(bn + 5 * 8).value:
+                dgrad += N * H * W * Cin // 8
+            if ptr(bn + 7 * 8).value:
+                dgrad += x
         if sym.startswith("conv_bwd_kernel"):
             return float(dgrad + wgrad - dy)   # dY read once by the fused launch
         if args[i0 - 5] is None:

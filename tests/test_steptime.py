@@ -43,3 +43,22 @@ def test_forward_bytes():
     r = (BF16, "x", "w", None, "o", 32, 56, 56, 64, 256, 1, 1, 1, 0, 56, 56, "sc", "sh", "res", None, None, 1, "s")
     assert ST.conv_bytes("conv2d_fwd_act", r, "conv_lds_kernel") == 2 * (M * 64 + 256 * 64 + 2 * M * 256)
     assert ST.conv_bytes("bn_act", r, "bn_act_kernel") is None
+
+
+def test_bn_reduce_epilogue_bytes():
+    """pose6d_conv2d_backward_chain_bn's epilogue also reads the BN's y (+ a second BN's
+    y2) and its ReLU bits: priced from the pose6d_bn_reduce_t the call passes."""
+    import ctypes
+
+    from pose6d.trunk import _BnReduce
+    sym = "conv_bwd_kernel<0, 2, 3>"
+    M = 32 * 56 * 56
+    x = M * 256 * 2
+    base = _bwd_args("conv2d_backward_chain_bn", BF16, "dres", "mask", "dx", 32, 56, 56, 256, 64, 1, 1, 56)
+    plain = ST.conv_bytes("conv2d_backward_chain_bn", base, sym)
+    one = _BnReduce(y=1, relu_mask=None, y2=None)
+    two = _BnReduce(y=1, relu_mask=1, y2=1)
+    a1 = base[:-2] + (ctypes.addressof(one), "st")
+    a2 = base[:-2] + (ctypes.addressof(two), "st")
+    assert ST.conv_bytes("conv2d_backward_chain_bn", a1, sym) == plain + x
+    assert ST.conv_bytes("conv2d_backward_chain_bn", a2, sym) == plain + 2 * x + M * 256 // 8
