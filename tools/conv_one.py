@@ -1,5 +1,5 @@
 """Run ONE conv pass of one shape a few times (PMC counter passes on a single kernel).
-usage: python tools/conv_one.py H W Cin Cout k s p [fwd|dgrad|bwd] [reps]"""
+usage: python tools/conv_one.py H W Cin Cout k s p [fwd|dgrad|wgrad|bwd] [reps]"""
 import os
 import sys
 
@@ -32,6 +32,9 @@ def main():
     for _ in range(reps):
         if ps == "fwd":
             call("conv2d_fwd", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, st)
+        elif ps == "wgrad":
+            call("conv2d_wgrad", dt, x, dy, dw, 0, ws, ws.numel() * 4, B, H, W, Cin, Cin, Cout, k, k, s, p, Ho, Wo,
+                 st)
         elif ps == "dgrad":
             call("conv2d_dgrad", dt, dy, wt, None, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, st)
         else:
