@@ -1049,30 +1049,39 @@ __global__ __launch_bounds__(64 * NW) void conv_lds_kernel(const T* __restrict__
   conv_lds_body<T, BM, BN, MODE, S, ACT, NW, BNR>(smem, blockIdx.x, src, wts, bias, res, out, stats, g);
 }
 
-// Fused backward of one conv: workgroups [0, nd) compute the data gradient,
-// [nd_pad, nd_pad + nw) the weight gradient (nd_pad = nd rounded up to 8 keeps
-// each part's XCD remap intact; the padding workgroups exit at once).  Both read
-// the same dY, and the weight-gradient workgroups fill the CUs the (often small)
-// data-gradient grid leaves idle -- one launch instead of two.
+// Fused backward of one conv.  Both passes read the same dY, and the weight-
+// gradient workgroups fill the CUs the (often small) data-gradient grid leaves idle
+// -- one launch instead of two.  Workgroup order = the order the dispatcher starts
+// them, longest work first (`wfirst`, chosen per conv by launch_bwd): with wfirst,
+// [0, nw) the weight gradient, [nw_pad, nw_pad + nd) the data gradient, else the data
+// gradient [0, nd) and the weight gradient [nd_pad, nd_pad + nw); the carried slab
+// reduce last.  (nw_pad / nd_pad round up to 8 so each part's XCD remap stays intact;
+// the padding workgroups exit at once.)  The weight-gradient workgroups of a 1x1
+// conv run ~10 K-steps; dispatched behind thousands of one- to four-step data-
+// gradient workgroups they were the launch's tail.
 template <int DMODE, int DS, int WS>
 __global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ wt,
                                                             const bf16* __restrict__ dres, bf16* __restrict__ dx,
-                                                            Geom gd, int nd, int nd_pad,
+                                                            Geom gd, int nd, int nd_pad, int wfirst,
                                                             const bf16* __restrict__ x, float* __restrict__ ws,
                                                             p6::WGeom gw, ReduceJob rj) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x;
   const int nw = gw.gm * gw.gn * gw.splits;
-  if (b < nd_pad) {
-    if (b < nd)
-      conv_lds_body<bf16, 64, 64, DMODE, DS, false, 4, true, true>(smem, b, dy, wt, nullptr, dres, dx, nullptr, gd);
-  } else if (b < nd_pad + nw) {
+  const int nw_pad = (nw + 7) & ~7;
+  const int d0 = wfirst ? nw_pad : 0;                  // first data-gradient workgroup
+  const int w0 = wfirst ? 0 : nd_pad;                  // first weight-gradient workgroup
+  const int r0 = wfirst ? nw_pad + nd : nd_pad + nw;   // first reduce workgroup
+  if (b >= d0 && b < d0 + nd) {
+    conv_lds_body<bf16, 64, 64, DMODE, DS, false, 4, true, true>(smem, b - d0, dy, wt, nullptr, dres, dx, nullptr,
+                                                                 gd);
+  } else if (b >= w0 && b < w0 + nw) {
     // kGemm data gradient <=> pointwise conv: the weight gradient takes the pointwise body
-    conv_wgrad_lds_body<64, 64, WS, DMODE == kGemm>(smem, b - nd_pad, x, dy, ws, gw);
-  } else {
+    conv_wgrad_lds_body<64, 64, WS, DMODE == kGemm>(smem, b - w0, x, dy, ws, gw);
+  } else if (b >= r0) {
     // the previous conv's weight-gradient slabs (another workspace), reduced here
     // instead of in a launch of their own
-    run_reduce_job(smem, b - nd_pad - nw, rj);
+    run_reduce_job(smem, b - r0, rj);
   }
 }
 
@@ -1539,8 +1548,13 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
   const int ring_w = WS * 128 * 128;
   int lds = ring_d > epi ? ring_d : epi;
   lds = lds > ring_w ? lds : ring_w;
-  conv_bwd_kernel<DMODE, DS, WS><<<nd_pad + nw + rj.nblk, kThreads, lds, s>>>(
-      (const bf16*)dy, (const bf16*)wt, (const bf16*)dres, (bf16*)dx, gd, nd, nd_pad, (const bf16*)x, ws, gw, rj);
+  // longest workgroups first: the weight gradient's K-steps per split against the
+  // data gradient's K-steps per tile
+  const int wfirst = p6::ceil_div(gw.mps, 64) >= nk;
+  const int grid = wfirst ? ((nw + 7) & ~7) + nd + rj.nblk : nd_pad + nw + rj.nblk;
+  conv_bwd_kernel<DMODE, DS, WS><<<grid, kThreads, lds, s>>>(
+      (const bf16*)dy, (const bf16*)wt, (const bf16*)dres, (bf16*)dx, gd, nd, nd_pad, wfirst, (const bf16*)x, ws, gw,
+      rj);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
