@@ -1550,7 +1550,10 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
   lds = lds > ring_w ? lds : ring_w;
   // longest workgroups first: the weight gradient's K-steps per split against the
   // data gradient's K-steps per tile
-  const int wfirst = p6::ceil_div(gw.mps, 64) >= nk;
+#ifndef POSE6D_BWD_ORDER
+#define POSE6D_BWD_ORDER 1   // build-time (A/B): 0 = the data gradient always first
+#endif
+  const int wfirst = POSE6D_BWD_ORDER && p6::ceil_div(gw.mps, 64) >= nk;
   const int grid = wfirst ? ((nw + 7) & ~7) + nd + rj.nblk : nd_pad + nw + rj.nblk;
   conv_bwd_kernel<DMODE, DS, WS><<<grid, kThreads, lds, s>>>(
       (const bf16*)dy, (const bf16*)wt, (const bf16*)dres, (bf16*)dx, gd, nd, nd_pad, wfirst, (const bf16*)x, ws, gw,

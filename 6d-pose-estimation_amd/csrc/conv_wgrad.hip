@@ -252,6 +252,9 @@ int tuned(const pose6d_tuning_t* t, int32_t pose6d_tuning_t::*f, int dflt) {
   return (t && t->*f >= 0) ? (int)(t->*f) : dflt;
 }
 
+#ifndef POSE6D_WGRAD_TARGET
+#define POSE6D_WGRAD_TARGET 256   // build-time (A/B sweeps): workgroups the bf16 split plan aims for
+#endif
 // bf16 weight gradients take the LDS-DMA kernel (64x64 tiles, 3-slot ring) unless a
 // pose6d_tuning_t (tests / tools only) asks for the register-staged kernel or another ring
 Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* tn = nullptr) {
@@ -266,10 +269,13 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
     p.stages = tuned(tn, &pose6d_tuning_t::wgrad_stages, 3);
     if (p.stages < 2) p.stages = 2;
     if (p.stages > 4) p.stages = 4;
-    // ~640 workgroups: fewer fp32 slabs to write and reduce than 1024, still ~2.5 per
-    // CU beside the data-gradient workgroups of the fused launch (end-to-end sweep:
-    // 384 / 512 / 640 / 1024 -> 5.24 / 5.16 / 5.14 / 5.20 ms per step)
-    target = 640;
+    // ~256 workgroups (one per CU): with the fused launch dispatching its longest
+    // workgroups first, long weight-gradient splits no longer form its tail, and
+    // fewer splits write and reduce fewer fp32 slabs.  End-to-end A/B on one box
+    // (profiles/r03w_wgrad_target_ab.txt): 256 / 384 / 448 / 512 / 640 / 896 / 1280 ->
+    // 4.64 / 4.70 / 4.65 / 4.65 / 4.71 / 4.81 / 4.89 ms per step (640 was the best
+    // target while the data gradient went first: 5.14 ms then, 384 -> 5.24)
+    target = POSE6D_WGRAD_TARGET;
     min_rows = 256;
     step = 64;
     max_bytes = 48ll << 20;

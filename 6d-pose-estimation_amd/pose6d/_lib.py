@@ -84,7 +84,9 @@ class Tuning(ctypes.Structure):
 
     @property
     def ref(self):
-        return ctypes.addressof(self)
+        # byref, not addressof: the argument object keeps the struct alive for the call,
+        # so `Tuning(...).ref` passed inline does not hand the library freed memory
+        return ctypes.byref(self)
 
 
 def symbols():
