@@ -1565,8 +1565,8 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
 template <int DMODE>
 int launch_bwd_mode(int ds, const Geom& gd, const p6::WGeom& gw, const void* dy, const void* wt, const void* dres,
                     void* dx, const void* x, float* ws, const ReduceJob& rj, hipStream_t s) {
-  return ds == 2 ? launch_bwd<DMODE, 2, 3>(gd, gw, dy, wt, dres, dx, x, ws, rj, s)
-                 : launch_bwd<DMODE, 4, 3>(gd, gw, dy, wt, dres, dx, x, ws, rj, s);
+  return ds == 2 ? launch_bwd<DMODE, 2, POSE6D_WGRAD_STAGES>(gd, gw, dy, wt, dres, dx, x, ws, rj, s)
+                 : launch_bwd<DMODE, 4, POSE6D_WGRAD_STAGES>(gd, gw, dy, wt, dres, dx, x, ws, rj, s);
 }
 
 }  // namespace
@@ -1578,7 +1578,8 @@ int launch_bwd_mode(int ds, const Geom& gd, const p6::WGeom& gw, const void* dy,
 // dx == NULL: weight gradient only.
 namespace {
 bool bwd_fused(const Plan& pd, const p6::WgradPlan& pw, const pose6d_tuning_t* tn) {
-  return pd.fast && pd.tile == 3 && (pd.stages == 2 || pd.stages == 4) && pw.fast && pw.stages == 3 &&
+  return pd.fast && pd.tile == 3 && (pd.stages == 2 || pd.stages == 4) && pw.fast &&
+         pw.stages == POSE6D_WGRAD_STAGES &&
          tune(tn, &pose6d_tuning_t::bwd_separate, 0) == 0;
 }
 

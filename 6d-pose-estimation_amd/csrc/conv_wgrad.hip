@@ -252,9 +252,18 @@ int tuned(const pose6d_tuning_t* t, int32_t pose6d_tuning_t::*f, int dflt) {
   return (t && t->*f >= 0) ? (int)(t->*f) : dflt;
 }
 
+// build-time (A/B sweeps): workgroups the bf16 / register-staged (fp32, stem) split
+// plans aim for, and the bf16 LDS ring depth
 #ifndef POSE6D_WGRAD_TARGET
-#define POSE6D_WGRAD_TARGET 256   // build-time (A/B sweeps): workgroups the bf16 split plan aims for
+#define POSE6D_WGRAD_TARGET 256
 #endif
+#ifndef POSE6D_WGRAD_TARGET_BASE
+#define POSE6D_WGRAD_TARGET_BASE 1024
+#endif
+#ifndef POSE6D_WGRAD_TARGET_F32
+#define POSE6D_WGRAD_TARGET_F32 512
+#endif
+
 // bf16 weight gradients take the LDS-DMA kernel (64x64 tiles, 3-slot ring) unless a
 // pose6d_tuning_t (tests / tools only) asks for the register-staged kernel or another ring
 Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* tn = nullptr) {
@@ -266,7 +275,7 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
   if (p.fast) {
     p.bm = 64;
     p.bn = 64;
-    p.stages = tuned(tn, &pose6d_tuning_t::wgrad_stages, 3);
+    p.stages = tuned(tn, &pose6d_tuning_t::wgrad_stages, POSE6D_WGRAD_STAGES);
     if (p.stages < 2) p.stages = 2;
     if (p.stages > 4) p.stages = 4;
     // ~256 workgroups (one per CU): with the fused launch dispatching its longest
@@ -282,7 +291,10 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
   } else {
     p.bm = Cout >= 128 ? 128 : 64;
     p.bn = Kpad >= 128 ? 128 : 64;
-    target = 1024;
+    // fp32 (all convs) / the bf16 stem; sweeps in profiles/r03x_wgrad_base_target_ab.txt:
+    // fp32 step 256 / 384 / 512 / 1024 / 2048 -> 13.73 / 13.63 / 13.04 / 13.36 / 13.38 ms,
+    // the bf16 step with 512 for its stem 4.665 vs 4.636 ms at 1024
+    target = dtype == POSE6D_DT_F32 ? POSE6D_WGRAD_TARGET_F32 : POSE6D_WGRAD_TARGET_BASE;
     min_rows = 256;
     step = MT;
     max_bytes = 64ll << 20;   // stem: 16 -> 64 MiB of slabs, 90 -> 65 us

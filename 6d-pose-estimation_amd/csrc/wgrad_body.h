@@ -5,6 +5,12 @@
 #include "common.h"
 #include "lds_dma.h"
 
+// LDS ring depth of the bf16 weight-gradient kernel (standalone and inside the fused
+// backward launch); build-time only, for A/B timing
+#ifndef POSE6D_WGRAD_STAGES
+#define POSE6D_WGRAD_STAGES 3
+#endif
+
 namespace p6 {
 
 struct WGeom {
