@@ -1071,7 +1071,7 @@ __global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const bf16* __restri
   const int nw_pad = (nw + 7) & ~7;
   const int d0 = wfirst ? nw_pad : 0;                  // first data-gradient workgroup
   const int w0 = wfirst ? 0 : nd_pad;                  // first weight-gradient workgroup
-  const int r0 = wfirst ? nw_pad + nd : nd_pad + nw;   // first reduce workgroup
+  const int r0 = wfirst ? nw_pad + nd : nd_pad + nw;   // first reduce workgroup (last: they fill the tail)
   if (b >= d0 && b < d0 + nd) {
     conv_lds_body<bf16, 64, 64, DMODE, DS, false, 4, true, true>(smem, b - d0, dy, wt, nullptr, dres, dx, nullptr,
                                                                  gd);

@@ -257,6 +257,9 @@ int tuned(const pose6d_tuning_t* t, int32_t pose6d_tuning_t::*f, int dflt) {
 #ifndef POSE6D_WGRAD_TARGET
 #define POSE6D_WGRAD_TARGET 256
 #endif
+#ifndef POSE6D_WGRAD_TARGET_KXK
+#define POSE6D_WGRAD_TARGET_KXK 256
+#endif
 #ifndef POSE6D_WGRAD_TARGET_BASE
 #define POSE6D_WGRAD_TARGET_BASE 1024
 #endif
@@ -284,7 +287,7 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
     // (profiles/r03w_wgrad_target_ab.txt): 256 / 384 / 448 / 512 / 640 / 896 / 1280 ->
     // 4.64 / 4.70 / 4.65 / 4.65 / 4.71 / 4.81 / 4.89 ms per step (640 was the best
     // target while the data gradient went first: 5.14 ms then, 384 -> 5.24)
-    target = POSE6D_WGRAD_TARGET;
+    target = Kpad == SC ? POSE6D_WGRAD_TARGET : POSE6D_WGRAD_TARGET_KXK;   // 1x1 / larger filters
     min_rows = 256;
     step = 64;
     max_bytes = 48ll << 20;
