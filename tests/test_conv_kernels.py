@@ -401,3 +401,20 @@ def test_pack_layouts(dtype, O, I, k, cpad):
     assert torch.equal(wp.float(), full.to(dtype).float())
     if I >= 8:
         assert torch.equal(wt.float(), w.permute(1, 2, 3, 0).to(dtype).float())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N,C,H,W,Cp", [(2, 3, 224, 224, 4), (3, 3, 7, 5, 4), (1, 4, 8, 8, 4), (2, 3, 6, 6, 8)])
+def test_nchw_to_nhwc(dtype, N, C, H, W, Cp):
+    """The model-input conversion (vectorised 4-pixel form when H*W % 4 == 0 and Cpad ==
+    4, per-element otherwise) equals torch's permute + zero channel padding exactly."""
+    from pose6d._lib import call, stream
+    from pose6d.trunk import DTYPES
+    x = torch.randn(N, C, H, W, generator=torch.Generator().manual_seed(3)).cuda()
+    y = torch.full((N, H, W, Cp), 7.0, device="cuda", dtype=dtype)
+    call("nchw_to_nhwc", DTYPES[dtype], x, y, N, C, H, W, Cp, stream())
+    ref = torch.zeros(N, H, W, Cp, dtype=dtype)
+    ref[..., :C] = x.cpu().permute(0, 2, 3, 1).to(dtype)
+    torch.cuda.synchronize()
+    assert torch.equal(y.cpu(), ref)
