@@ -1600,9 +1600,29 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
   };
   P6_CHECK_ARG(phases >= 1 && phases <= 3, "pose6d_conv2d_backward_ex: phases must be 1, 2 or 3");
   P6_CHECK_ARG(!bnr || (dx && phases == 3), "pose6d_conv2d_backward: a BatchNorm reduce needs the data gradient");
+  // chain mode with a register-staged weight gradient (fp32, the bf16 stem): that launch
+  // carries the previous conv's slab reduce as trailing workgroups and leaves its own
+  // reduce pending, as the fused bf16 launch does -- one launch per conv fewer
+  auto carry_wgrad = [&](bool& carried) -> int {
+    carried = false;
+    if (!deferred || phases != 3) return POSE6D_OK;
+    p6::WgradPlan pw;
+    const p6::WGeom gw = p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw, tn);
+    if (pw.fast) return POSE6D_OK;
+    P6_CHECK_ARG((int64_t)pw.splits * Cout * gw.Kpad * 4 <= ws_bytes,
+                 "pose6d_conv2d_backward: workspace %lld bytes < %lld needed", (long long)ws_bytes,
+                 (long long)pw.splits * Cout * gw.Kpad * 4);
+    const int rc = p6::wgrad_launch_carry(dtype, gw, pw, x, dy, workspace, rj ? *rj : none, p6::stream_of(stream));
+    carried = rc == POSE6D_OK;
+    *deferred = carried;
+    return rc;
+  };
   if (dx == nullptr) {
     if (!(phases & 1)) return POSE6D_OK;
-    const int rc = flush_prev();
+    bool carried;
+    int rc = carry_wgrad(carried);
+    if (rc || carried) return rc;
+    rc = flush_prev();
     if (rc) return rc;
     return pose6d_conv2d_wgrad_tuned(dtype, x, dy, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real, Cout,
                                      KH, KW, stride, pad, Ho, Wo, tn, stream);
@@ -1620,11 +1640,19 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
   const bool fused = bwd_fused(pd, pw, tn);
   if (!fused) {
     if (!(phases & 1)) return POSE6D_OK;
-    int rc = flush_prev();
+    const bool carry = deferred && phases == 3 && !pw.fast;
+    int rc = carry ? POSE6D_OK : flush_prev();
     if (rc) return rc;
     rc = dgrad_impl(dtype, dy, wt, dres, dres_mask, dx, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, stream, tn,
                     bnr);
     if (rc) return rc;
+    if (carry) {
+      bool carried;
+      rc = carry_wgrad(carried);
+      if (rc || carried) return rc;
+      rc = flush_prev();
+      if (rc) return rc;
+    }
     return pose6d_conv2d_wgrad_tuned(dtype, x, dy, dw, accumulate, workspace, ws_bytes, N, H, W, Cin, Cin_real, Cout,
                                      KH, KW, stride, pad, Ho, Wo, tn, stream);
   }

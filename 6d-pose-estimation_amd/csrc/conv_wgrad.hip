@@ -58,7 +58,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* img, int col, int grp, int
 
 template <typename T, int BM, int BN>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy,
-                                                              float* __restrict__ ws, WGeom g) {
+                                                              float* __restrict__ ws, WGeom g, ReduceJob rj) {
   constexpr int VEC = WT<T>::VEC;
   constexpr bool BF = sizeof(T) == 2;
   constexpr int YROW = BM * (int)sizeof(T);   // bytes per LDS row of the dY image
@@ -72,6 +72,10 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const T* __restric
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tiles = g.gm * g.gn;
+  if ((int)blockIdx.x >= tiles * g.splits) {   // trailing workgroups: the carried reduce
+    run_reduce_job(smem, blockIdx.x - tiles * g.splits, rj);
+    return;
+  }
   const int split = blockIdx.x / tiles;
   int t2 = blockIdx.x - split * tiles;
   const int tm = t2 / g.gn, tn = t2 - tm * g.gn;
@@ -333,20 +337,23 @@ int launch_fast(const WGeom& g, const void* x, const void* dy, float* ws, hipStr
 }
 
 template <typename T, int BM, int BN>
-int launch(const WGeom& g, const void* x, const void* dy, float* ws, hipStream_t s) {
+int launch(const WGeom& g, const void* x, const void* dy, float* ws, hipStream_t s, const ReduceJob& rj) {
   const int ring = 2 * MT * (BM + BN) * (int)sizeof(T);
-  const int lds = ring > acc_stage_bytes<BM, BN>() ? ring : acc_stage_bytes<BM, BN>();
-  conv_wgrad_kernel<T, BM, BN><<<g.gm * g.gn * g.splits, kThreads, lds, s>>>((const T*)x, (const T*)dy, ws, g);
+  int lds = ring > acc_stage_bytes<BM, BN>() ? ring : acc_stage_bytes<BM, BN>();
+  if (lds < 256 * 16) lds = 256 * 16;   // the carried reduce's 256 float4
+  conv_wgrad_kernel<T, BM, BN><<<g.gm * g.gn * g.splits + rj.nblk, kThreads, lds, s>>>((const T*)x, (const T*)dy,
+                                                                                        ws, g, rj);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
 
 template <typename T>
-int launch_any(const WGeom& g, int bm, int bn, const void* x, const void* dy, float* ws, hipStream_t s) {
-  if (bm == 128 && bn == 128) return launch<T, 128, 128>(g, x, dy, ws, s);
-  if (bm == 128) return launch<T, 128, 64>(g, x, dy, ws, s);
-  if (bn == 128) return launch<T, 64, 128>(g, x, dy, ws, s);
-  return launch<T, 64, 64>(g, x, dy, ws, s);
+int launch_any(const WGeom& g, int bm, int bn, const void* x, const void* dy, float* ws, hipStream_t s,
+               const ReduceJob& rj = ReduceJob{}) {
+  if (bm == 128 && bn == 128) return launch<T, 128, 128>(g, x, dy, ws, s, rj);
+  if (bm == 128) return launch<T, 128, 64>(g, x, dy, ws, s, rj);
+  if (bn == 128) return launch<T, 64, 128>(g, x, dy, ws, s, rj);
+  return launch<T, 64, 64>(g, x, dy, ws, s, rj);
 }
 
 int ilog2(int v) {
@@ -391,6 +398,13 @@ WGeom wgrad_geom(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int 
 int wgrad_reduce_launch(const float* ws, float* dw, int Cout, int Kpad, int SC, int Cin, int KH, int KW, int splits,
                         int accumulate, hipStream_t s) {
   return launch_reduce(ws, dw, Cout, Kpad, SC, Cin, KH, KW, splits, accumulate, s);
+}
+
+int wgrad_launch_carry(int dtype, const WGeom& g, const WgradPlan& p, const void* x, const void* dy, float* ws,
+                       const ReduceJob& rj, hipStream_t s) {
+  P6_CHECK_ARG(!p.fast, "wgrad_launch_carry: register-staged plans only");
+  return dtype == POSE6D_DT_BF16 ? launch_any<bf16>(g, p.bm, p.bn, x, dy, ws, s, rj)
+                                 : launch_any<float>(g, p.bm, p.bn, x, dy, ws, s, rj);
 }
 
 }  // namespace p6

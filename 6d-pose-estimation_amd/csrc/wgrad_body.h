@@ -26,11 +26,24 @@ struct WgradPlan {
   int bm, bn, splits, mps, stages;
 };
 
+// a slab reduce carried by another launch (the next conv's backward: the fused bf16
+// launch or the register-staged weight gradient), nblk extra workgroups
+struct ReduceJob {
+  const float* ws;
+  float* dw;
+  int Cout, Kpad, SC, Cin, KH, KW, splits, accumulate, G, nblk;
+};
+
 // defined in conv_wgrad.hip
 WGeom wgrad_geom(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad, int Ho,
                  int Wo, WgradPlan* plan, const pose6d_tuning_t* tuning = nullptr);
 int wgrad_reduce_launch(const float* ws, float* dw, int Cout, int Kpad, int SC, int Cin, int KH, int KW, int splits,
                         int accumulate, hipStream_t s);
+// the register-staged weight gradient of plan `p` (not p.fast) with the carried
+// reduce `rj` as its trailing workgroups; its own slabs are left for the caller to
+// reduce (carried by the next launch or pose6d_wgrad_reduce)
+int wgrad_launch_carry(int dtype, const WGeom& g, const WgradPlan& p, const void* x, const void* dy, float* ws,
+                       const ReduceJob& rj, hipStream_t s);
 
 }  // namespace p6
 
@@ -412,12 +425,7 @@ __device__ __forceinline__ void wgrad_reduce_body(float4* red, int blk, const fl
   }
 }
 
-// a slab reduce carried by another launch (the next conv's fused backward)
-struct ReduceJob {
-  const float* ws;
-  float* dw;
-  int Cout, Kpad, SC, Cin, KH, KW, splits, accumulate, G, nblk;
-};
+using p6::ReduceJob;
 
 __host__ __device__ inline int reduce_group(int splits) { return splits >= 64 ? 16 : splits >= 16 ? 4 : 1; }
 __host__ __device__ inline int reduce_blocks(int Cout, int Kpad, int G) {
