@@ -5,6 +5,7 @@
 OUT=$1; VAR=$2; ROUNDS=${3:-3}
 CMD="python bench.py --steps 40 --warmup 10 --no-side --no-fp32 --no-cpu-baseline --no-kernel-profile"
 [ "${4:-}" = "fp32" ] && CMD="python tools/fp32_step.py"
+[ "${4:-}" = "eval" ] && CMD="python tools/eval_time.py"
 mkdir -p $OUT
 for r in $(seq 1 $ROUNDS); do
   timeout -k 10 200 $CMD > $OUT/ab_base_$r.json 2>/dev/null || exit 1
