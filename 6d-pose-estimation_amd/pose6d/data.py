@@ -47,18 +47,34 @@ class TrainAugment:
     transforms.RandomErasing(p, scale, ratio, value=0) of the reference's
     train_transform (train_rgbd_geometric.py:41-47), as pose6d_crop_rgbd_train runs
     them.  Each call of the owning CropRGBD draws fresh parameters: the kernel seed is
-    (seed, calls so far) -- deterministic for a given seed and call sequence."""
+    (seed, rank, calls so far) -- deterministic for a given seed, rank and call sequence.
+
+    `rank` (default: the torch.distributed rank when a process group is initialised,
+    else 0) is mixed into every kernel seed, so that data-parallel ranks sharing one
+    `seed` draw different jitter / erase parameters for their crop b (the reference's
+    DataLoader workers draw from independent torch RNG streams).  Rank 0 keeps the
+    single-process sequence.  The seed reaches the kernel as a by-value argument:
+    do not capture a CropRGBD(augment=...) call into a hipGraph -- a replay would
+    repeat the captured call's parameters."""
 
     def __init__(self, brightness=0.3, contrast=0.3, saturation=0.3, hue=0.05, erase_p=0.2, erase_scale=(0.02, 0.1),
-                 erase_ratio=(0.3, 3.3), seed=0):
+                 erase_ratio=(0.3, 3.3), seed=0, rank=None):
         self.jitter = (float(brightness), float(contrast), float(saturation), float(hue))
         self.erase = (float(erase_p), float(erase_scale[0]), float(erase_scale[1]), float(erase_ratio[0]),
                       float(erase_ratio[1]))
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        if rank is None:
+            import torch.distributed as dist
+            rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+        self.rank = int(rank)
         self.calls = 0
 
     def next_seed(self):
-        s = (self.seed * 0x9E3779B97F4A7C15 + self.calls * 0xD1B54A32D192ED03 + 1) & 0xFFFFFFFFFFFFFFFF
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            raise Pose6dError("TrainAugment: the augmented crop must not be graph-captured (its seed is a "
+                              "by-value kernel argument: every replay would repeat the same parameters)")
+        s = (self.seed * 0x9E3779B97F4A7C15 + self.calls * 0xD1B54A32D192ED03 + 1
+             + self.rank * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
         self.calls += 1
         return s
 

@@ -64,14 +64,25 @@ def resnet50_trunk(in_channels=3):
     return seq
 
 
+class PretrainedWeightsUnavailable(RuntimeError):
+    """pretrained=True without local ImageNet weights (the reference's
+    resnet50(weights=ResNet50_Weights.DEFAULT) raises when the download fails)."""
+
+
 def load_pretrained(seq):
-    """ImageNet weights (torchvision ResNet50_Weights.DEFAULT) cannot be downloaded
-    here; if POSE6D_RESNET50_WEIGHTS names a local torchvision resnet50 state_dict
-    it is loaded (weights_only), otherwise the trunk keeps its random init."""
+    """ImageNet weights (torchvision ResNet50_Weights.DEFAULT, pose_net_rgbd_geometric.py:23-25)
+    cannot be downloaded here; POSE6D_RESNET50_WEIGHTS must name a local torchvision
+    resnet50 state_dict (loaded weights_only).  Without one this raises, as the
+    reference does when its download is impossible, so that an unchanged training
+    script cannot silently train from random init; POSE6D_ALLOW_RANDOM_INIT=1 opts
+    into the random init explicitly (a warning is still emitted)."""
     path = os.environ.get("POSE6D_RESNET50_WEIGHTS")
     if not path or not os.path.exists(path):
-        warnings.warn("pretrained=True: no local ResNet50 ImageNet weights (set POSE6D_RESNET50_WEIGHTS); "
-                      "using random init", RuntimeWarning, stacklevel=3)
+        msg = ("pretrained=True: no local ResNet50 ImageNet weights (set POSE6D_RESNET50_WEIGHTS to a torchvision "
+               "resnet50 state_dict, or POSE6D_ALLOW_RANDOM_INIT=1 to train from random init)")
+        if os.environ.get("POSE6D_ALLOW_RANDOM_INIT", "") not in ("1", "true", "yes"):
+            raise PretrainedWeightsUnavailable(msg + (f"; {path!r} does not exist" if path else ""))
+        warnings.warn(msg + ": using random init", RuntimeWarning, stacklevel=3)
         return False
     sd = torch.load(path, map_location="cpu", weights_only=True)
     names = {"conv1": "0", "bn1": "1", "layer1": "4", "layer2": "5", "layer3": "6", "layer4": "7"}

@@ -91,8 +91,11 @@ class RGBDGeometricTrainer:
         # hp[6]: gradient scale read by adamw_step -- 1/world averages the all-reduced sum
         # inside the update (exact for power-of-two world sizes: scaling by 2^-k commutes
         # with every rounding; arena.grad then holds the SUM after a step).  Other world
-        # sizes average the gradient in a pass of their own first, as torch DDP does
-        # (g_sum * (1/world) rounded once, then clipped), and hp[6] stays 1.
+        # sizes average the all-reduced SUM in a pass of their own before the clip
+        # (g_sum * (1/world), rounded once), and hp[6] stays 1.  That is a post-all-reduce
+        # average: torch DDP's Reducer pre-scales each rank's gradient by 1/world before
+        # the all-reduce, so for non-power-of-two worlds the two differ in the last bit.
+        # The reference trains on one GPU (no DDP), so this rounding is parity unpinned.
         self._avg_pass = self.world > 1 and (self.world & (self.world - 1)) != 0
         scale = 1.0 if (self.world == 1 or self._avg_pass) else 1.0 / self.world
         self.hp = torch.tensor([lr, betas[0], betas[1], eps, weight_decay, 0.0, scale, max_norm],
@@ -142,7 +145,7 @@ class RGBDGeometricTrainer:
     def _optimizer(self):
         st = stream()
         if self._avg_pass:
-            self.arena.grad.mul_(1.0 / self.world)   # torch DDP's average (non power-of-two world)
+            self.arena.grad.mul_(1.0 / self.world)   # post-all-reduce average (non power-of-two world)
         # (world > 1: the 1/world average of the all-reduced gradient is hp[6], applied
         # inside adamw_step; the norm partials see the sum, scaled there too)
         # step counter hp[5] += 1 and dropout seed += 1 ride on the norm-partials launch

@@ -14,7 +14,6 @@ Prints ONE JSON line on rank 0 (contract in the task statement), including
 rank 0 only, bounded sample).
 """
 import argparse
-import glob
 import json
 import os
 import sys
@@ -40,6 +39,11 @@ PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X fp32 MFMA peak = the vector rate (MI355X
 # 2048-2048-1024-512-{4,3} heads (13.64 M multiply-adds)
 RGB_FWD_FLOPS_PER_CROP = 8.175e9 + 2 * 13_635_072
 ADD_FLOPS_PER_PAIR = 8.0       # 3 sub, 1 mul, 2 fma per ADD-S pair
+# The committed PMC passes (tools/pmc_round.sh + tools/pmc_summary.py: separate FETCH_SIZE /
+# WRITE_SIZE / SQ_VALU_MFMA_BUSY_CYCLES runs, FETCH_SIZE doubled for gfx950) the roofline
+# `traffic` field is read from: one explicit file per compute dtype, updated in the commit
+# that adds a newer pass (never picked by file-name order).  --pmc-bf16 / --pmc-f32 override.
+PMC_SUMMARY = {"bf16": "profiles/r03f_pmc.json", "f32": "profiles/r03u_f32_pmc.json"}
 
 
 def synth_batch(B, dev, seed):
@@ -172,7 +176,13 @@ def main():
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
     ap.add_argument("--no-side", action="store_true", help="skip the configs[1] / configs[3] side measurements")
     ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 (reference precision) training line")
+    ap.add_argument("--pmc-bf16", default=None, help="PMC summary json for the bf16 roofline traffic")
+    ap.add_argument("--pmc-f32", default=None, help="PMC summary json for the fp32 roofline traffic")
     args = ap.parse_args()
+    if args.pmc_bf16:
+        PMC_SUMMARY["bf16"] = args.pmc_bf16
+    if args.pmc_f32:
+        PMC_SUMMARY["f32"] = args.pmc_f32
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -273,10 +283,15 @@ def kernel_profile(tr, data, step_ms, peak_tflops=None, with_forward=True, reps=
     from pose6d import steptime
     if peak_tflops is None:
         peak_tflops = PEAK_BF16_TFLOPS if tr.trunk.dtype == torch.bfloat16 else PEAK_F32_MFMA_TFLOPS
+    # the instrumented replays run whole AdamW steps: keep the trainer's state as the
+    # timed loop left it (weights, moments, step counter / hyper-parameters, dropout seed)
+    snap = tr.snapshot()
     timer = steptime.StepTimer(lambda: tr.step_body(data), tr.dev)
     recs = timer.run(reps, plain_ms=step_ms)
     inst_ms = timer.total_ms
     timer.close()
+    tr.restore(snap)
+    torch.cuda.synchronize()
     agg = steptime.by_symbol(recs)
     conv = {k: v for k, v in agg.items() if v["flops_known"] and v["flops"] > 0}
     sym, a = max(conv.items(), key=lambda kv: kv[1]["time_us"])
@@ -284,7 +299,7 @@ def kernel_profile(tr, data, step_ms, peak_tflops=None, with_forward=True, reps=
     achieved = a["flops"] / a["launches"] / avg_t / 1e12
     conv_total_ms = sum(v["time_us"] for v in conv.values()) * 1e-3
     busy_ms = sum(r["us"] for r in recs) * 1e-3
-    pmc, tsrc = pmc_traffic(sym)
+    pmc, tsrc = pmc_traffic(sym, "bf16" if tr.trunk.dtype == torch.bfloat16 else "f32")
     traffic = round(pmc["hbm_bytes_per_launch"]) if pmc else None
     # SQ_VALU_MFMA_BUSY_CYCLES summed over the chip's 1024 SIMDs; busy fraction at 2.4 GHz
     mfma_busy = (round(pmc["mfma_busy_cycles_per_launch"] / (avg_t * 2.4e9 * 1024), 4)
@@ -370,25 +385,27 @@ def fp32_train(dev, steps, warmup, B=32):
         tr.step(data)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / steps * 1e3
+    loss = float(tr.loss.item())   # read before the instrumented replays
     kp = kernel_profile(tr, data, ms, PEAK_F32_MFMA_TFLOPS, with_forward=False)
     return {"workload": "PoseNetRGBDGeometric train step, bs32 224^2, fp32 end to end (the reference's precision), "
                         "fused RGBDGeometricTrainer, hipGraph replay",
             "value": round(B / (ms * 1e-3), 2), "unit": "crops/s", "ms_per_step": round(ms, 4), "steps": steps,
-            "dtype": "f32", "loss": float(tr.loss.item()), **kp}
+            "dtype": "f32", "loss": loss, **kp}
 
 
-def pmc_traffic(sym):
-    """HBM bytes per launch of `sym` from the newest committed PMC summary
-    (profiles/*pmc*.json, made by tools/pmc_round.sh + tools/pmc_summary.py:
-    separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled for gfx950)."""
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
-        try:
-            k = json.load(open(f))["kernels"].get(sym)
-        except (OSError, ValueError, KeyError):
-            continue
-        if k and "hbm_bytes_per_launch" in k:
-            return k, os.path.relpath(f, REPO)
-    return None, None
+def pmc_traffic(sym, dtype):
+    """HBM bytes per launch of `sym` from the committed PMC summary named for this
+    compute dtype in PMC_SUMMARY (made by tools/pmc_round.sh + tools/pmc_summary.py:
+    separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled for gfx950).  None when
+    that file has no entry for the symbol (a kernel the pass predates)."""
+    f = os.path.join(REPO, PMC_SUMMARY[dtype])
+    try:
+        k = json.load(open(f))["kernels"].get(sym)
+    except (OSError, ValueError, KeyError):
+        return None, PMC_SUMMARY[dtype]
+    if k and "hbm_bytes_per_launch" in k:
+        return k, PMC_SUMMARY[dtype]
+    return None, PMC_SUMMARY[dtype]
 
 
 def _time_fn(fn, reps):

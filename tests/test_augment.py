@@ -178,3 +178,15 @@ def test_train_transform_parameter_distributions():
     assert area.min() > 0.015 and area.max() < 0.11
     assert (h / w).min() > 0.25 and (h / w).max() < 3.6
     assert (er[:, 8] + h <= 224).all() and (er[:, 9] + w <= 224).all() and (er[:, 8:10] >= 0).all()
+
+
+def test_train_augment_seed_depends_on_rank():
+    """Data-parallel ranks with one user seed draw different parameters (the rank is
+    mixed into every kernel seed); rank 0 keeps the single-process sequence."""
+    from pose6d.data import TrainAugment
+    r0, r1, r0b = TrainAugment(seed=7, rank=0), TrainAugment(seed=7, rank=1), TrainAugment(seed=7)
+    s0 = [r0.next_seed() for _ in range(4)]
+    s1 = [r1.next_seed() for _ in range(4)]
+    assert s0 == [r0b.next_seed() for _ in range(4)]   # no process group: rank 0
+    assert len(set(s0) | set(s1)) == 8
+    assert s0[0] == (7 * 0x9E3779B97F4A7C15 + 1) & 0xFFFFFFFFFFFFFFFF

@@ -44,6 +44,44 @@ def test_structure_matches_reference(name):
     assert sd[f"{pre}.0.weight"].shape == (64, 3, 7, 7)
 
 
+@pytest.mark.parametrize("name", list(EXPECTED))
+def test_pretrained_without_weights_raises(name, monkeypatch, tmp_path):
+    """pretrained=True (the reference scripts' default) must not silently fall back to
+    random init: the reference raises when ResNet50_Weights.DEFAULT cannot be fetched."""
+    from pose6d.resnet import PretrainedWeightsUnavailable
+    monkeypatch.delenv("POSE6D_RESNET50_WEIGHTS", raising=False)
+    monkeypatch.delenv("POSE6D_ALLOW_RANDOM_INIT", raising=False)
+    with pytest.raises(PretrainedWeightsUnavailable):
+        _models()[name](pretrained=True)
+    monkeypatch.setenv("POSE6D_RESNET50_WEIGHTS", str(tmp_path / "missing.pth"))
+    with pytest.raises(PretrainedWeightsUnavailable, match="does not exist"):
+        _models()[name](pretrained=True)
+    # explicit opt-in: random init with a warning
+    monkeypatch.setenv("POSE6D_ALLOW_RANDOM_INIT", "1")
+    with pytest.warns(RuntimeWarning, match="random init"):
+        _models()[name](pretrained=True)
+
+
+def test_pretrained_loads_local_torchvision_state_dict(monkeypatch, tmp_path):
+    """POSE6D_RESNET50_WEIGHTS: a torchvision-named resnet50 state_dict lands in the trunk."""
+    from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
+    from pose6d.resnet import resnet50_trunk
+    torch.manual_seed(3)
+    seq = resnet50_trunk()
+    names = {"0": "conv1", "1": "bn1", "4": "layer1", "5": "layer2", "6": "layer3", "7": "layer4"}
+    tv = {}
+    for k, v in seq.state_dict().items():
+        head = k.split(".")[0]
+        tv[names[head] + k[len(head):]] = v
+    tv["fc.weight"], tv["fc.bias"] = torch.zeros(1000, 2048), torch.zeros(1000)
+    path = tmp_path / "resnet50.pth"
+    torch.save(tv, path)
+    monkeypatch.setenv("POSE6D_RESNET50_WEIGHTS", str(path))
+    m = PoseNetRGBDGeometric(pretrained=True)
+    assert torch.equal(m.backbone[0].weight, seq[0].weight)
+    assert torch.equal(m.backbone[7][2].conv3.weight, seq[7][2].conv3.weight)
+
+
 def _oracle_forward(name, P, inputs, training):
     if name == "PoseNetRGB":
         return OR.forward_rgb(P, inputs["rgb"], training)

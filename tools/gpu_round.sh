@@ -12,5 +12,5 @@ timeout -k 10 600 python bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err 
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/prof_$TAG.log 2>&1
 echo "prof rc=$?" >> $OUT/prof_$TAG.log
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/roof_$TAG -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --roofline-only > $OUT/roof_$TAG.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/roof_$TAG -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --no-side --no-fp32 --no-cpu-baseline > $OUT/roof_$TAG.log 2>&1
 echo "roof rc=$?" >> $OUT/roof_$TAG.log
