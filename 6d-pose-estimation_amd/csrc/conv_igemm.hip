@@ -73,7 +73,79 @@ struct Geom {
   const float *bnr_mean2, *bnr_inv2;
   float* bnr_part2;
   int bnr_rows;
+  // split-K (LDS-DMA path, kGemm / kFwd / kDgrad): each output tile's K-steps are
+  // divided over `splits` workgroups (0 or 1 = none); see splitk_merge
+  int splits;
 };
+
+// ---------------------------------------------------------------------------
+// Split-K inside one launch.  The small-grid layers (layer3/4 at batch 32: a few
+// hundred 64x64 tiles, 16-72 K-steps each) are bound by the operand bytes a CU
+// keeps in flight, not by MFMA: bigger tiles move fewer bytes per MAC but leave CUs
+// idle unless the K range of a tile is shared by several workgroups.  Each split
+// writes its fp32 partial tile write-through (buffer stores with sc1), waits for
+// them (vmcnt(0)), and after a workgroup barrier one lane adds 1 to the tile's
+// arrival counter (agent scope); the workgroup whose add returns splits-1 is the
+// last: it re-arms the counter, reads the other partials with sc1 buffer loads
+// (after a barrier) and sums ALL partials in split order p0 + p1 + ... (its own from
+// registers) -- one summation order per plan, whoever arrives last -- then runs the
+// normal epilogue (bias, BN statistics, act, residual).  No workgroup waits for
+// another, so residency does not matter.  This is the hand-off MI355X_MICROARCH.md
+// measures valid with sc1 stores and loads in place of release / acquire fences.
+// The partials and counters are one library-owned device buffer: split-K launches on
+// one device must be stream-ordered (every launch re-arms the counters it used).
+constexpr int64_t kSkWsFloats = (48ll << 20) / 4;   // 48 MiB of partial tiles
+constexpr int kSkMaxTiles = 8192;
+__device__ float g_sk_ws[kSkWsFloats];
+__device__ int g_sk_cnt[kSkMaxTiles];
+
+// the partials of `tiles` tiles x `splits` fit the buffer (host-side plan check)
+inline bool splitk_fits(int64_t tiles, int splits, int tile_elems) {
+  return splits > 1 && tiles <= kSkMaxTiles && tiles * splits * tile_elems <= kSkWsFloats;
+}
+
+// TM x TN accumulator tiles per wave; PART = floats of one (tile, split) partial
+template <int TM, int TN, int NW>
+__device__ __forceinline__ bool splitk_merge(f32x4 (&acc)[TM][TN], char* smem, int tile, int split, int nsplit) {
+  constexpr int PART = NW * TM * TN * 64 * 4;
+  constexpr int SC1 = 16;   // buffer cache-policy bits: sc1
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* base = g_sk_ws + (int64_t)tile * nsplit * PART;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, nsplit * PART * 4, 0x00020000);
+  const int voff = (wave * TM * TN * 64 + lane) * 16;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
+                                             voff + (i * TN + j) * 1024, split * PART * 4, SC1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave, before the barrier
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem);
+  if (tid == 0) flag[0] = __hip_atomic_fetch_add(&g_sk_cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const bool last = flag[0] == nsplit - 1;
+  __syncthreads();   // flag read by every wave before the epilogue reuses the LDS
+  if (!last) return false;
+  if (tid == 0) __hip_atomic_store(&g_sk_cnt[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  f32x4 mine[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) mine[i][j] = acc[i][j];
+  for (int s = 0; s < nsplit; ++s) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const f32x4 v = s == split ? mine[i][j]
+                                   : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                   rs, voff + (i * TN + j) * 1024, s * PART * 4, SC1));
+        acc[i][j] = s == 0 ? v : acc[i][j] + v;
+      }
+  }
+  return true;
+}
 
 // LDS bytes the BN-reduce epilogue needs beyond the staged tile: per wave, per chunk
 // column, (sum dz, sum dz xhat, sum dz xhat2) x 16-byte chunk = 12 bytes per column,
@@ -763,13 +835,22 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   constexpr int SA = BM * 128, STAGE = (BM + BN) * 128;
   static_assert(S >= 2, "ring needs two stages");
 
+  constexpr bool SK = MODE == kGemm || MODE == kFwd || MODE == kDgrad;   // split-K capable modes
+  const int nsplit = SK && g.splits > 1 ? g.splits : 1;
   const int per = g.gm * g.gn;
-  const int nwg = MODE == kDgradS2 ? s2_classes(g) * per : per;
+  const int nwg = (MODE == kDgradS2 ? s2_classes(g) * per : per) * nsplit;
   int bid = bid_in;
   {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
+  // split-K: the splits of one tile are consecutive logical ids (one XCD, mostly)
+  int split = 0;
+  if (nsplit > 1) {
+    split = bid % nsplit;
+    bid /= nsplit;
+  }
+  const int tile_id = bid;
   // parity class (kDgradS2): the four classes of one tile are consecutive logical
   // ids, so every XCD gets an even share of the heavy and the empty classes and the
   // four blocks that gather the same dY rows run on the same L2
@@ -936,6 +1017,23 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
     }
   };
 
+  // split-K: this workgroup's K-steps [kb, ke) of the tile; the tap walk starts at kb
+  if (SK && nsplit > 1) {
+    const int kb = (int)((int64_t)split * nk / nsplit), ke = (int)((int64_t)(split + 1) * nk / nsplit);
+    nk = ke - kb;
+    if (MODE == kGemm) {
+      c0 = kb << LOG_KS;
+    } else {
+      const int spt = g.SC >> LOG_KS;   // K-steps per filter tap
+      const int tap = kb / spt;
+      c0 = (kb - tap * spt) << LOG_KS;
+      kh = tap / g.KW;
+      kw = tap - kh * g.KW;
+      tap_koff = tap * g.SC;
+    }
+    if (c0 != 0) set_tap();   // issue() rebuilds the row pointers only at a tap start
+  }
+
   f32x4 acc[TM][TN];
   f32x4 acc2[DUAL ? TM : 1][DUAL ? TN : 1];   // kGemmDual: the block GEMM's sums, parked
 #pragma unroll
@@ -1032,6 +1130,9 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
     wbuf = wbuf == S - 1 ? 0 : wbuf + 1;
   }
   asm volatile("s_barrier" ::: "memory");   // every wave done reading the ring before the epilogue reuses it
+  if constexpr (SK) {
+    if (nsplit > 1 && !splitk_merge<TM, TN, NW>(acc, smem, tile_id, split, nsplit)) return;
+  }
   if constexpr (DUAL)   // acc2 = the block GEMM, acc = the downsample branch
     conv_epilogue<T, BM, BN, 1, NW, true>(acc2, smem, g, bias, nullptr, out, nullptr, m0, n0, -1, acc, pre, false);
   else
@@ -1116,7 +1217,10 @@ int launch_fast(const Geom& g0, const void* src, const void* w, const float* bia
   const int epi = (MODE == kGemmDual ? 2 : 1) * BM * (BN * (int)sizeof(T) + 16) + (g.bnr_part ? bnr_lds(NW, BN) : 0);
   const int lds = ring > epi ? ring : epi;
   if (MODE == kDgradS2) s2_single_class(g, res, out);
-  const int grid = g.gm * g.gn * (MODE == kDgradS2 ? s2_classes(g) : 1);
+  constexpr bool SK = MODE == kGemm || MODE == kFwd || MODE == kDgrad;
+  if (!SK || !splitk_fits(g.gm * g.gn, g.splits, BM * BN)) g.splits = 1;
+  if (g.splits > nk) g.splits = nk > 0 ? nk : 1;
+  const int grid = g.gm * g.gn * (MODE == kDgradS2 ? s2_classes(g) : 1) * (g.splits > 1 ? g.splits : 1);
   if constexpr (MODE == kGemm || MODE == kFwd || MODE == kGemmDual) {
     if (g.act) {   // eval BN-act epilogue (pose6d_conv2d_fwd_act)
       conv_lds_kernel<T, BM, BN, MODE, S, true, NW><<<grid, 64 * NW, lds, s>>>(
@@ -1338,6 +1442,8 @@ Plan choose(int dtype, int mode, const Geom& g, bool fused = false, const pose6d
   if (p.stages > 6) p.stages = 6;
   if (p.stages == 5) p.stages = 4;
   if (cols128 && rows128 && p.stages > 4) p.stages = 4;   // 6 x 32 KiB exceeds the 160 KiB LDS
+  p.g.splits = tune(tn, &pose6d_tuning_t::conv_splitk, 1);
+  if (fused || !(p.mode == kGemm || p.mode == kFwd || p.mode == kDgrad) || p.g.splits < 1) p.g.splits = 1;
   return p;
 }
 

@@ -251,9 +251,11 @@ int pose6d_conv2d_backward(int32_t dtype, const void *x, const void *dy, const v
  *   conv_base     1: the register-staged conv kernels instead of the LDS-DMA path
  *   wgrad_stages  LDS ring slots of the bf16 weight-gradient kernel (2..4)
  *   wgrad_base    1: the register-staged weight-gradient kernel (other split plan)
- *   bwd_separate  1: data and weight gradient as separate launches (not the fused kernel) */
+ *   bwd_separate  1: data and weight gradient as separate launches (not the fused kernel)
+ *   conv_splitk   fast path (1x1 / KxK forward, stride-1 data gradient): K-steps of each output tile
+ *                 split over this many workgroups of one launch (1 = none) */
 typedef struct {
-  int32_t conv_tile, conv_stages, conv_s2, conv_base, wgrad_stages, wgrad_base, bwd_separate;
+  int32_t conv_tile, conv_stages, conv_s2, conv_base, wgrad_stages, wgrad_base, bwd_separate, conv_splitk;
 } pose6d_tuning_t;
 int pose6d_conv2d_fwd_tuned(int32_t dtype, const void *x, const void *w, const float *bias, void *y, float *stats,
                             int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW,

@@ -1,6 +1,8 @@
 """Worker of tests/test_ddp_gpu.py (launched by torch.distributed.run, 2 or 3 ranks on
 ONE GPU over gloo: RCCL needs a GPU per rank; 3 ranks exercise the non-power-of-two
-average pass).  Each rank trains one step on its
+average pass).  argv: OUT [B [BUCKET_MB]] -- B = 4 with 2 MB buckets (many buckets and
+segments on a small model step), or BASELINE configs[4]'s per-rank workload: B = 32 with
+the trainer's default 25 MB buckets (what bench.py --gpus N builds).  Each rank trains one step on its
 OWN batch (seed 77 + rank) through the bucketed all-reduce path
 (RGBDGeometricTrainer with a process group), eagerly and replayed from the
 segmented graphs.  Rank 0 also builds the expected update in one process: the
@@ -27,10 +29,11 @@ def main():
     from bench import synth_batch
     from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
     from pose6d.train import RGBDGeometricTrainer
-    B = 4
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+    bucket = float(sys.argv[3]) if len(sys.argv) > 3 else 2.0
     batches = [synth_batch(B, dev, seed=77 + r) for r in range(world)]
 
-    def trainer(pg, bucket_mb=2.0):
+    def trainer(pg, bucket_mb=bucket):
         torch.manual_seed(0)
         model = PoseNetRGBDGeometric(pretrained=False).to(dev)
         for m in model.modules():

@@ -192,6 +192,78 @@ def test_conv_fast_variants_bit_identical(cfg):
     _close(dxb, dx0, 2e-2, "dgrad base vs LDS-DMA")
 
 
+SPLITK_CONFIGS = [
+    (4, 14, 14, 1024, 256, 1, 1, 0),   # layer3 1x1 reduce (GEMM mode, K = 16 steps)
+    (4, 7, 7, 512, 512, 3, 1, 1),      # layer4 3x3 (implicit GEMM, 72 steps, taps split mid-way)
+    (2, 14, 14, 256, 256, 3, 2, 1),    # 3x3 / s2 forward (its data gradient: parity classes, not split)
+    (3, 7, 7, 2048, 512, 1, 1, 0),     # layer4 1x1 reduce, M = 147 (partial last row tile)
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cfg", SPLITK_CONFIGS)
+def test_conv_splitk(cfg, dtype):
+    """Split-K inside one launch (pose6d_tuning_t.conv_splitk): each tile's K-steps over
+    several workgroups, partials merged by the last arriver in split order.  Against
+    the torch fp32 op (forward, BN statistics, data gradient + residual); for one split
+    count every tile / ring depth gives the same bits (the sum order depends on the
+    split count only), and a repeated launch reproduces them (the arrival counters
+    re-arm themselves)."""
+    from pose6d._lib import Tuning, call, query, stream
+    from pose6d.trunk import DTYPES, pack_single
+    N, H, W, Cin, Cout, k, s, p = cfg
+    g = torch.Generator().manual_seed(11)
+    dev = "cuda"
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, k, k, generator=g) * (2.0 / (Cin * k * k)) ** 0.5
+    dy = torch.randn(N, Cout, Ho, Wo, generator=g)
+    dres = torch.randn(N, Cin, H, W, generator=g)
+    if dtype == torch.bfloat16:
+        x, w, dy, dres = (t.bfloat16().float() for t in (x, w, dy, dres))
+    xr = x.clone().requires_grad_(True)
+    yr = F.conv2d(xr, w, None, stride=s, padding=p)
+    yr.backward(dy)
+    dt = DTYPES[dtype]
+    xd, dyd, dresd = _nhwc(x).to(dev, dtype), _nhwc(dy).to(dev, dtype), _nhwc(dres).to(dev, dtype)
+    wp, wt = pack_single(w.to(dev), Cin, dtype)
+    rows = query("conv_stats_rows", N, Ho, Wo, Cout)
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+
+    def run(**kw):
+        tn = Tuning(**kw)
+        y = torch.empty(N, Ho, Wo, Cout, device=dev, dtype=dtype)
+        st = torch.empty(2, Cout, rows, device=dev)
+        dx = torch.empty(N, H, W, Cin, device=dev, dtype=dtype)
+        call("conv2d_fwd_tuned", dt, xd, wp, None, y, st, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, tn.ref, stream())
+        call("conv2d_dgrad_tuned", dt, dyd, wt, dresd, dx, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, tn.ref,
+             stream())
+        torch.cuda.synchronize()
+        return y.cpu(), st.cpu(), dx.cpu()
+
+    for splits in (1, 2, 3, 4, 7):
+        ref = None
+        for tile in (3, 4, 0):
+            for stages in (2, 4):
+                got = run(conv_splitk=splits, conv_tile=tile, conv_stages=stages)
+                if ref is None:
+                    ref = got
+                    y, st, dx = got
+                    _close(y.permute(0, 3, 1, 2), yr.detach(), tol, f"fwd splits={splits}")
+                    _close(dx.permute(0, 3, 1, 2), xr.grad + dres, tol, f"dgrad splits={splits}")
+                    # the statistics rows of the epilogue: per-32-row sums add up to the column sums
+                    ysum = yr.detach().double().sum((0, 2, 3))
+                    _close(st[0].double().sum(1), ysum, 1e-3 if dtype == torch.float32 else 2e-2,
+                           f"stats sum splits={splits}")
+                else:
+                    for a, b, what in zip(ref, got, ("fwd", "stats", "dgrad")):
+                        assert torch.equal(a, b), f"{what}: splits={splits} tile={tile} stages={stages} differs"
+        again = run(conv_splitk=splits)
+        for a, b, what in zip(ref, again, ("fwd", "stats", "dgrad")):
+            assert torch.equal(a, b), f"{what}: repeated launch differs (splits={splits})"
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("C,N,H", [(64, 4, 9), (32, 2, 7), (256, 8, 33)])

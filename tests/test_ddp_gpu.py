@@ -13,13 +13,16 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_ddp_bucketed_step_matches_mean_gradient_update(world):
+@pytest.mark.parametrize("world,batch,bucket_mb", [(2, 4, 2.0), (3, 4, 2.0), (2, 32, 25.0)],
+                         ids=["w2-b4", "w3-b4", "w2-b32-configs4"])
+def test_ddp_bucketed_step_matches_mean_gradient_update(world, batch, bucket_mb):
+    """w2-b32-configs4: BASELINE configs[4]'s per-rank workload -- bs32 per rank, bf16,
+    the default 25 MB gradient buckets and the segmented graphs bench.py --gpus N builds."""
     out = os.path.join(tempfile.mkdtemp(), "ddp")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr", "127.0.0.1", "--master-port", str(29631 + world),
-           os.path.join(REPO, "tests", "ddp_worker.py"), out]
+           "--master-addr", "127.0.0.1", "--master-port", str(29631 + world + batch),
+           os.path.join(REPO, "tests", "ddp_worker.py"), out, str(batch), str(bucket_mb)]
     r = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     for rank in range(world):
@@ -31,3 +34,24 @@ def test_ddp_bucketed_step_matches_mean_gradient_update(world):
         assert graph_same == "1", f"rank {rank}: graph-segmented DDP step != eager DDP step"
         assert run_eager == "1" and run_graph == "1", f"rank {rank}: local BN running stats differ"
         assert agree == "1", "ranks hold different parameters"
+
+
+@pytest.mark.gpu
+def test_bench_world2_json_line():
+    """bench.py's N > 1 path end to end (configs[4] per rank: bs32, 25 MB buckets,
+    segmented graphs), 2 ranks sharing the box's one GPU over gloo
+    (POSE6D_BENCH_SHARE_GPU=1; RCCL needs a GPU per rank): the JSON line reports the
+    whole job -- n_gpus 2, global batch 64, value = 64 crops x steps / max-over-ranks time."""
+    import json
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", POSE6D_BENCH_SHARE_GPU="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", "29671", os.path.join(REPO, "bench.py"), "--gpus", "2",
+           "--steps", "3", "--warmup", "1", "--no-side", "--no-fp32", "--no-cpu-baseline", "--no-kernel-profile"]
+    r = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 64 and res["config"]["per_gpu_batch"] == 32
+    assert res["config"]["parallelism"] == "dp2" and res["scaling"] == "weak"
+    assert res["value"] > 0 and abs(res["value"] - 64 * 1e3 / res["ms_per_step"]) < 1e-3 * res["value"] + 0.1
