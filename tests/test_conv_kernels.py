@@ -406,6 +406,116 @@ def test_backward_masked_residual(cfg, dtype):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_backward_chain_carried_reduce(dtype):
+    """pose6d_conv2d_backward_chain over three convs as the trunk issues them: each call
+    may leave its weight-gradient slab reduce pending (*deferred) for the next call to
+    run as trailing workgroups (`prev`, ping-pong workspaces) -- the fp32 LDS-DMA and
+    register-staged weight gradients carry it too, and a stem-shaped conv (Cin 4,
+    dx = NULL) closes the chain.  dX and dW must equal separate pose6d_conv2d_backward
+    calls bit for bit (the reduce is the same launch body, only moved)."""
+    import ctypes
+    from pose6d._lib import Tuning, call, query, stream
+    from pose6d.trunk import DTYPES, _WgradReduce, pack_single
+    g = torch.Generator().manual_seed(21)
+    dev, dt = "cuda", DTYPES[dtype]
+    N = 2
+    convs = [  # (H, W, Cin, Cin_real, Cout, k, s, p, has dgrad)
+        (14, 14, 256, 256, 256, 3, 1, 1, True),
+        (14, 14, 128, 128, 256, 1, 1, 0, True),
+        (32, 32, 4, 3, 64, 7, 2, 3, False),
+    ]
+    ops = []
+    wsz = 0
+    for (H, W, Cin, Cr, Cout, k, s, p, dg) in convs:
+        Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        x = torch.randn(N, Cin, H, W, generator=g)
+        x[:, Cr:] = 0.0   # the padded input channels (stem: RGB padded to 4)
+        x = _nhwc(x).to(dev, dtype)
+        w = (torch.randn(Cout, Cr, k, k, generator=g) * 0.05).to(dev)
+        wp, wt = pack_single(w, Cin, dtype, with_t=dg)
+        dy = _nhwc(torch.randn(N, Cout, Ho, Wo, generator=g)).to(dev, dtype)
+        ops.append((H, W, Cin, Cr, Cout, k, s, p, dg, Ho, Wo, x, wt, dy))
+        wsz = max(wsz, query("conv2d_wgrad_workspace", dt, N, Ho, Wo, Cin, Cout, k, k))
+    # separate calls: the reference -- as one conv2d_backward each, and as data and
+    # weight gradient in separate launches (the fused launch must match them bit for bit)
+    ref = []
+    ws = torch.empty(wsz // 4 + 1, device=dev)
+    for (H, W, Cin, Cr, Cout, k, s, p, dg, Ho, Wo, x, wt, dy) in ops:
+        outs = []
+        for sep in (0, 1):
+            dx = torch.empty(N, H, W, Cin, device=dev, dtype=dtype) if dg else None
+            dw = torch.empty(Cout, Cr, k, k, device=dev)
+            call("conv2d_backward_tuned", dt, x, dy, wt if dg else None, None, dx, dw, 0, ws, ws.numel() * 4, N, H, W,
+                 Cin, Cr, Cout, k, k, s, p, Ho, Wo, Tuning(bwd_separate=sep).ref, stream())
+            torch.cuda.synchronize()
+            outs.append((dx.clone() if dg else None, dw.clone()))
+        if dg:
+            assert torch.equal(outs[0][0], outs[1][0]), f"fused vs separate dX differ {(H, Cin, Cout, k)}"
+        assert torch.equal(outs[0][1], outs[1][1]), f"fused vs separate dW differ {(H, Cin, Cout, k)}"
+        ref.append(outs[0])
+    # the chain
+    ws_pp = (torch.empty(wsz // 4 + 1, device=dev), torch.empty(wsz // 4 + 1, device=dev))
+    slot, pending, keep = 0, None, []
+    deferred = ctypes.c_int32(0)
+    got = []
+    for (H, W, Cin, Cr, Cout, k, s, p, dg, Ho, Wo, x, wt, dy) in ops:
+        ws = ws_pp[slot]
+        dx = torch.full((N, H, W, Cin), float("nan"), device=dev, dtype=dtype) if dg else None
+        dw = torch.full((Cout, Cr, k, k), float("nan"), device=dev)
+        call("conv2d_backward_chain", dt, x, dy, wt if dg else None, None, dx, dw, 0, ws, ws.numel() * 4, N, H, W,
+             Cin, Cr, Cout, k, k, s, p, Ho, Wo, ctypes.addressof(pending) if pending is not None else None,
+             ctypes.addressof(deferred), stream())
+        got.append((dx, dw))
+        if deferred.value:
+            pending = _WgradReduce(ws.data_ptr(), dw.data_ptr(), dt, N, H, W, Cin, Cr, Cout, k, k, s, p, Ho, Wo, 0)
+            keep.append(pending)
+            slot ^= 1
+        else:
+            pending = None
+    if pending is not None:
+        call("wgrad_reduce", ctypes.addressof(pending), stream())
+    torch.cuda.synchronize()
+    for i, ((rdx, rdw), (gdx, gdw)) in enumerate(zip(ref, got)):
+        if rdx is not None:
+            assert torch.equal(rdx, gdx), f"conv {i}: chained dX differs"
+        assert torch.equal(rdw, gdw), f"conv {i}: chained dW differs"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_wgrad_fast_vs_register_staged(dtype):
+    """The LDS-DMA weight gradient (bf16 and, since round 4, fp32) against the
+    register-staged kernel (Tuning(wgrad_base=1)) and the torch op: other split plans
+    sum the pixels in another order, so close, not equal; a stride-2 3x3, a partial
+    last split and a 1x1 with more than one k tile."""
+    from pose6d._lib import Tuning, call, query, stream
+    from pose6d.trunk import DTYPES
+    g = torch.Generator().manual_seed(5)
+    dev, dt = "cuda", DTYPES[dtype]
+    for (N, H, W, Cin, Cout, k, s, p) in [(2, 28, 28, 128, 128, 3, 2, 1), (3, 15, 15, 64, 128, 3, 1, 1),
+                                          (2, 14, 14, 256, 192, 1, 1, 0), (2, 28, 28, 64, 256, 1, 2, 0)]:
+        Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        x = torch.randn(N, Cin, H, W, generator=g)
+        dyt = torch.randn(N, Cout, Ho, Wo, generator=g)
+        if dtype == torch.bfloat16:
+            x, dyt = x.bfloat16().float(), dyt.bfloat16().float()
+        ref = torch.nn.grad.conv2d_weight(x.double(), (Cout, Cin, k, k), dyt.double(), stride=s, padding=p)
+        xd, dyd = _nhwc(x).to(dev, dtype), _nhwc(dyt).to(dev, dtype)
+        outs = []
+        for tn in (Tuning(), Tuning(wgrad_base=1)):
+            ws = torch.empty(query("conv2d_wgrad_workspace_tuned", dt, N, Ho, Wo, Cin, Cout, k, k, tn.ref) // 4 + 1,
+                             device=dev)
+            dw = torch.empty(Cout, Cin, k, k, device=dev)
+            call("conv2d_wgrad_tuned", dt, xd, dyd, dw, 0, ws, ws.numel() * 4, N, H, W, Cin, Cin, Cout, k, k, s, p,
+                 Ho, Wo, tn.ref, stream())
+            torch.cuda.synchronize()
+            outs.append(dw.cpu())
+        _close(outs[0], ref.float(), 1e-4, f"wgrad fast {(H, Cin, Cout, k, s)}")
+        _close(outs[1], ref.float(), 1e-4, f"wgrad base {(H, Cin, Cout, k, s)}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_pools(dtype):
     from pose6d._lib import call, stream
     from pose6d.trunk import DTYPES

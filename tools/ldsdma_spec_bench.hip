@@ -92,17 +92,137 @@ __global__ __launch_bounds__(64 * (NP + NC)) void loop_kernel(const char* __rest
         const int chunk = (cw * RPW + r) * 64 + lane;   // 16-B chunk of the slot
         f[r] = *reinterpret_cast<const u32x4*>(src + (chunk % (SLOT * 64)) * 16);
       }
+      if constexpr (MF >= 0) {
 #pragma unroll
-      for (int m = 0; m < MF; ++m)
-        acc[m & 3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f[m % RPW]),
-                                                             __builtin_bit_cast(bf16x8, f[(m + 1) % RPW]), acc[m & 3],
-                                                             0, 0, 0);
+        for (int m = 0; m < MF; ++m)
+          acc[m & 3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f[m % RPW]),
+                                                               __builtin_bit_cast(bf16x8, f[(m + 1) % RPW]),
+                                                               acc[m & 3], 0, 0, 0);
+      } else {   // fp32: -MF exact v_mfma_f32_16x16x4_f32 (32 cycles each)
+#pragma unroll
+        for (int m = 0; m < -MF; ++m)
+          acc[m & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(__builtin_bit_cast(f32x4, f[m % RPW])[m & 3],
+                                                            __builtin_bit_cast(f32x4, f[(m + 1) % RPW])[m & 3],
+                                                            acc[m & 3], 0, 0, 0);
+      }
     }
     cur = cur == S - 1 ? 0 : cur + 1;
     wb = wb == S - 1 ? 0 : wb + 1;
   }
   const float v = acc[0][0] + acc[1][1] + acc[2][2] + acc[3][3];
   if (v == 12345.f) sink[blockIdx.x * blockDim.x + threadIdx.x] = v;
+}
+
+// lgkmcnt(0) that the compiler sees as redefining the fragment registers
+// (and, named as operands too, after the MFMAs that produce `acc`: otherwise hipcc
+// may sink those MFMAs below the wait and the reads stop overlapping them)
+template <int N>
+__device__ __forceinline__ void lgkm_wait(u32x4 (&f)[N], f32x4 (&acc)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])::"memory");
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(f[i]));
+}
+
+// software-pipelined uniform loop: after the barrier that publishes stage st+1, every
+// wave issues the fragment reads of stage st+1 and then the MFMAs of stage st (its
+// fragments already in registers), so the LDS reads overlap the matrix work; the
+// slot of stage st (read completely before that barrier) is refilled right away
+template <int NW, int SLOT, int S, int RPW, int MF>
+__global__ __launch_bounds__(64 * NW) void pipe_kernel(const char* __restrict__ buf, size_t mask, int steps, int stride,
+                                                       float* __restrict__ sink) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int PER = SLOT / NW;
+  static_assert(PER * NW == SLOT, "slot must split over the waves");
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const size_t wg_base = (size_t)blockIdx.x * 977 * 1024;
+  const int rowoff = (lane >> 3) * stride + (lane & 7) * 16;
+  auto issue = [&](int st, int slot) {
+    char* dst = smem + slot * SLOT * 1024;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int piece = i * NW + wave;
+      const size_t off = (wg_base + (size_t)st * SLOT * 1024 + (size_t)piece * 8 * stride + rowoff) & mask;
+      glds16(buf + off, dst + piece * 1024);
+    }
+  };
+  // fragment reads as inline asm (no wait): hipcc neither orders them behind the
+  // in-flight LDS-DMA (vmcnt(0)) nor waits for them before unrelated MFMAs; the
+  // explicit lgkm_wait below (operands named "+v") releases them
+  const unsigned ring = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
+  auto read = [&](u32x4 (&f)[RPW], int slot) {
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const int chunk = (wave * RPW + r) * 64 + lane;
+      const unsigned a = ring + slot * SLOT * 1024 + (chunk % (SLOT * 64)) * 16;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(f[r]) : "v"(a));
+    }
+  };
+  f32x4 acc[4] = {};
+  for (int s = 0; s < S - 1 && s < steps; ++s) issue(s, s);
+  wait_j<PER, S - 2>(steps - 1 < S - 2 ? steps - 1 : S - 2);   // stage 0 landed
+  asm volatile("s_barrier" ::: "memory");
+  u32x4 fa[RPW], fb[RPW];
+  read(fa, 0);
+  lgkm_wait<RPW>(fa, acc);
+  int slot = 0;
+  for (int st = 0; st < steps; st += 2) {
+    // two iterations per trip so the fragment buffers alternate without copies
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int s_ = st + h;
+      if (s_ >= steps) break;
+      u32x4 (&cur)[RPW] = h == 0 ? fa : fb;
+      u32x4 (&nxt)[RPW] = h == 0 ? fb : fa;
+      // issued so far: stages 0 .. min(s_+S-2, steps-1); stage s_+1 must have landed
+      const int hi = s_ + S - 2 < steps - 1 ? s_ + S - 2 : steps - 1;
+      const int left = hi - (s_ + 1);
+      if (s_ + 1 < steps) wait_j<PER, (S >= 3 ? S - 3 : 0)>(left < 0 ? 0 : left);
+      asm volatile("s_barrier" ::: "memory");
+      const int nslot = slot == S - 1 ? 0 : slot + 1;
+      if (s_ + S - 1 < steps) issue(s_ + S - 1, slot == 0 ? S - 1 : slot - 1);
+      if (s_ + 1 < steps) read(nxt, nslot);
+#pragma unroll
+      for (int m = 0; m < MF; ++m)
+        acc[m & 3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, cur[m % RPW]),
+                                                             __builtin_bit_cast(bf16x8, cur[(m + 1) % RPW]),
+                                                             acc[m & 3], 0, 0, 0);
+      lgkm_wait<RPW>(nxt, acc);
+      slot = nslot;
+    }
+  }
+  const float v = acc[0][0] + acc[1][1] + acc[2][2] + acc[3][3];
+  if (v == 12345.f) sink[blockIdx.x * blockDim.x + threadIdx.x] = v;
+}
+
+template <int NW, int SLOT, int S, int RPW, int MF>
+void run_pipe(const char* buf, size_t foot, int wpc, float* sink, const char* name) {
+  constexpr int lds = S * SLOT * 1024;
+  if (lds * wpc > 160 * 1024 || 64 * NW * wpc > 2048) return;
+  const int grid = 256 * wpc, steps = 64, stride = 2048;
+  auto k = pipe_kernel<NW, SLOT, S, RPW, MF>;
+  CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int w = 0; w < 3; ++w) k<<<grid, 64 * NW, lds>>>(buf, foot - 1, steps, stride, sink);
+  CK(hipGetLastError());
+  const int reps = 10;
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) k<<<grid, 64 * NW, lds>>>(buf, foot - 1, steps, stride, sink);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  const double t = ms * 1e-3 / reps;
+  const double per_step_ns = t / steps * 1e9;
+  const double mfma_cyc = (double)MF * 16 * NW * wpc / 4;
+  printf("%-12s NW=%d slot=%2dK S=%d RPW=%2d MF=%2d wpc=%d : %7.2f us  %6.1f ns/stage  %6.1f GB/s/CU  "
+         "MFMA %5.1f%% of the stage (2.4 GHz)\n",
+         name, NW, SLOT, S, RPW, MF, wpc, t * 1e6, per_step_ns / wpc, (double)grid * steps * SLOT * 1024 / t / 256 / 1e9,
+         100.0 * mfma_cyc / (per_step_ns * 2.4));
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
 }
 
 template <int NP, int NC, int SLOT, int S, int RPW, int MF>
@@ -127,7 +247,7 @@ void run(const char* buf, size_t foot, int wpc, float* sink, const char* name) {
   CK(hipEventElapsedTime(&ms, e0, e1));
   const double t = ms * 1e-3 / reps;
   const double per_step_ns = t / steps * 1e9;
-  const double mfma_cyc = (double)MF * 16 * NC * wpc / 4;   // per SIMD per stage (16x16x32: 16 cycles)
+  const double mfma_cyc = (MF >= 0 ? (double)MF * 16 : -(double)MF * 32) * NC * wpc / 4;   // per SIMD per stage
   printf("%-12s NP=%d NC=%d slot=%2dK S=%d RPW=%2d MF=%2d wpc=%d : %7.2f us  %6.1f ns/stage  %6.1f GB/s/CU  "
          "MFMA %5.1f%% of the stage (2.4 GHz)\n",
          name, NP, NC, SLOT, S, RPW, MF, wpc, t * 1e6, per_step_ns / wpc, (double)grid * steps * SLOT * 1024 / t / 256 / 1e9,
@@ -143,6 +263,35 @@ int main() {
   CK(hipMalloc(&buf, (size_t)64 << 20));
   CK(hipMemset(buf, 0, (size_t)64 << 20));
   CK(hipMalloc(&sink, 1 << 24));
+  // fp32 64x64 tile (4 waves of 32x32: 32 exact 16x16x4 MFMAs + 8 reads per wave per 16 KiB stage)
+  run<0, 4, 16, 3, 8, -32>(buf, foot, 1, sink, "f32uni64");
+  run<0, 4, 16, 3, 8, -32>(buf, foot, 2, sink, "f32uni64");
+  run<4, 4, 16, 3, 8, -32>(buf, foot, 1, sink, "f32spec64");
+  run<4, 4, 16, 4, 8, -32>(buf, foot, 1, sink, "f32spec64");
+  run<2, 4, 16, 4, 8, -32>(buf, foot, 1, sink, "f32spec64");
+  run<4, 4, 16, 3, 8, -32>(buf, foot, 2, sink, "f32spec64");
+  run<4, 8, 32, 3, 12, -32>(buf, foot, 1, sink, "f32spec128");
+  run<0, 8, 32, 3, 12, -32>(buf, foot, 1, sink, "f32uni128");
+  run<0, 4, 16, 3, 8, -32>(buf, foot, 3, sink, "f32uni64");
+  run<0, 4, 16, 3, 1, -32>(buf, foot, 1, sink, "f32uni64lowLDS");
+  // two K-steps per barrier (32 KiB stages, 64 MFMAs + 16 reads per wave)
+  run<0, 4, 32, 2, 16, -64>(buf, foot, 1, sink, "f32uni64x2");
+  run<0, 4, 32, 2, 16, -64>(buf, foot, 2, sink, "f32uni64x2");
+  run<0, 4, 32, 3, 16, -64>(buf, foot, 1, sink, "f32uni64x2");
+  run<0, 4, 64, 2, 32, -128>(buf, foot, 1, sink, "f32uni64x4");
+  run<0, 8, 64, 2, 24, -64>(buf, foot, 1, sink, "f32uni128x2");
+  run<0, 4, 32, 2, 16, 16>(buf, foot, 1, sink, "bf16uni64x2");
+  run<0, 4, 32, 2, 16, 16>(buf, foot, 2, sink, "bf16uni64x2");
+  run<4, 4, 16, 3, 1, -32>(buf, foot, 1, sink, "f32spec64lowLDS");
+  run_pipe<8, 32, 3, 12, 16>(buf, foot, 1, sink, "pipe128");
+  run_pipe<8, 32, 4, 12, 16>(buf, foot, 1, sink, "pipe128");
+  run_pipe<4, 32, 3, 16, 32>(buf, foot, 1, sink, "pipe128w4");
+  run_pipe<4, 32, 4, 16, 32>(buf, foot, 1, sink, "pipe128w4");
+  run_pipe<4, 16, 3, 8, 8>(buf, foot, 1, sink, "pipe64");
+  run_pipe<4, 16, 3, 8, 8>(buf, foot, 2, sink, "pipe64");
+  run_pipe<8, 48, 3, 16, 32>(buf, foot, 1, sink, "pipe256x128");
+  run_pipe<8, 32, 3, 12, 0>(buf, foot, 1, sink, "pipe128noMF");
+  run_pipe<8, 32, 3, 1, 16>(buf, foot, 1, sink, "pipe128lowLDS");
   // 64x64 tile, 4 waves of 32x32 (today's default): 16 KiB stages, 8 reads + 8 MFMAs per wave
   run<0, 4, 16, 2, 8, 8>(buf, foot, 1, sink, "uni64x64");
   run<0, 4, 16, 2, 8, 8>(buf, foot, 2, sink, "uni64x64");
