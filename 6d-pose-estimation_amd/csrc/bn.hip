@@ -54,14 +54,14 @@ __device__ __forceinline__ void store_vec(T* p, const float* f) {
 // S1^2/N small against S2 (K is a mean of the same data): no E[x^2]-E[x]^2
 // cancellation.
 template <int L>
-__global__ __launch_bounds__(kThreads) void bn_stats_finalize_kernel(
-    const float* __restrict__ part, int rows, int C, int64_t M, const float* __restrict__ gamma,
+__device__ __forceinline__ void bn_stats_finalize_body(
+    int blk, const float* __restrict__ part, int rows, int C, int64_t M, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
     float momentum, float eps, float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ smean,
     float* __restrict__ sinv) {
   __shared__ double red[2][kThreads / 64];
   const int lane = threadIdx.x % L;
-  const int c = blockIdx.x * (kThreads / L) + threadIdx.x / L;
+  const int c = blk * (kThreads / L) + threadIdx.x / L;
   double s1 = 0.0, s2 = 0.0, K = 0.0;
   // the per-channel parameters and running statistics the tail needs, fetched now
   // so their round trip overlaps the partial-row reduction instead of following it
@@ -131,6 +131,28 @@ __global__ __launch_bounds__(kThreads) void bn_stats_finalize_kernel(
     rvar[c] = (1.f - momentum) * rv_c + momentum * (float)unb;
     if (c == 0 && nbt) nbt[0] += 1;
   }
+}
+
+template <int L>
+__global__ __launch_bounds__(kThreads) void bn_stats_finalize_kernel(
+    const float* __restrict__ part, int rows, int C, int64_t M, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
+    float momentum, float eps, float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ smean,
+    float* __restrict__ sinv) {
+  bn_stats_finalize_body<L>(blockIdx.x, part, rows, C, M, gamma, beta, rmean, rvar, nbt, momentum, eps, scale, shift,
+                            smean, sinv);
+}
+
+// two BatchNorms over the same output grid (a downsampling block's bn3 and its
+// downsample BN: same rows and count) in one launch, blockIdx.y selecting the BN;
+// each BN's arithmetic is bn_stats_finalize_kernel<L>'s, bit for bit
+template <int L>
+__global__ __launch_bounds__(kThreads) void bn_stats_finalize2_kernel(pose6d_bn_stats_t a, pose6d_bn_stats_t b,
+                                                                      int rows, int64_t M) {
+  const pose6d_bn_stats_t& d = blockIdx.y ? b : a;
+  if ((int)blockIdx.x * (kThreads / L) >= d.C) return;
+  bn_stats_finalize_body<L>(blockIdx.x, d.partial, rows, d.C, M, d.gamma, d.beta, d.running_mean, d.running_var,
+                            d.num_batches, d.momentum, d.eps, d.scale, d.shift, d.save_mean, d.save_invstd);
 }
 
 // eval: running statistics -> scale / shift / saved mean / invstd (no partials)
@@ -533,6 +555,20 @@ extern "C" int pose6d_bn_finalize(const float* partial, int32_t rows, int32_t C,
     bn_eval_finalize_kernel<<<p6::ceil_div(C, kThreads), kThreads, 0, s>>>(gamma, beta, running_mean, running_var, C,
                                                                           eps, scale, shift, save_mean, save_invstd);
   }
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+extern "C" int pose6d_bn_finalize_dual(const pose6d_bn_stats_t* a, const pose6d_bn_stats_t* b, int32_t rows,
+                                       int64_t count, void* stream) {
+  P6_CHECK_ARG(a && b && a->C > 0 && b->C > 0 && rows > 0 && count > 0 && rows == p6::ceil_div(count, (int64_t)32),
+               "pose6d_bn_finalize_dual: bad sizes");
+  hipStream_t s = p6::stream_of(stream);
+  const int cmax = a->C > b->C ? a->C : b->C;
+  if (rows > 512)
+    bn_stats_finalize2_kernel<256><<<dim3(cmax, 2), kThreads, 0, s>>>(*a, *b, rows, count);
+  else
+    bn_stats_finalize2_kernel<64><<<dim3(p6::ceil_div(cmax, 4), 2), kThreads, 0, s>>>(*a, *b, rows, count);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }

@@ -1160,11 +1160,13 @@ __global__ __launch_bounds__(64 * NW) void conv_lds_kernel(const T* __restrict__
 // the padding workgroups exit at once.)  The weight-gradient workgroups of a 1x1
 // conv run ~10 K-steps; dispatched behind thousands of one- to four-step data-
 // gradient workgroups they were the launch's tail.
-template <int DMODE, int DS, int WS>
-__global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ wt,
-                                                            const bf16* __restrict__ dres, bf16* __restrict__ dx,
+// T = float: the same launch for the reference-precision (fp32) step -- the fp32
+// LDS-DMA data gradient and the fp32 LDS-DMA weight gradient (wgrad_body.h).
+template <int DMODE, int DS, int WS, typename T = bf16>
+__global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ wt,
+                                                            const T* __restrict__ dres, T* __restrict__ dx,
                                                             Geom gd, int nd, int nd_pad, int wfirst,
-                                                            const bf16* __restrict__ x, float* __restrict__ ws,
+                                                            const T* __restrict__ x, float* __restrict__ ws,
                                                             p6::WGeom gw, ReduceJob rj) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x;
@@ -1174,11 +1176,13 @@ __global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const bf16* __restri
   const int w0 = wfirst ? 0 : nd_pad;                  // first weight-gradient workgroup
   const int r0 = wfirst ? nw_pad + nd : nd_pad + nw;   // first reduce workgroup (last: they fill the tail)
   if (b >= d0 && b < d0 + nd) {
-    conv_lds_body<bf16, 64, 64, DMODE, DS, false, 4, true, true>(smem, b - d0, dy, wt, nullptr, dres, dx, nullptr,
-                                                                 gd);
+    conv_lds_body<T, 64, 64, DMODE, DS, false, 4, true, true>(smem, b - d0, dy, wt, nullptr, dres, dx, nullptr, gd);
   } else if (b >= w0 && b < w0 + nw) {
     // kGemm data gradient <=> pointwise conv: the weight gradient takes the pointwise body
-    conv_wgrad_lds_body<64, 64, WS, DMODE == kGemm>(smem, b - w0, x, dy, ws, gw);
+    if constexpr (sizeof(T) == 2)
+      conv_wgrad_lds_body<64, 64, WS, DMODE == kGemm>(smem, b - w0, x, dy, ws, gw);
+    else
+      conv_wgrad_lds_body_f32<64, WS, DMODE == kGemm>(smem, b - w0, x, dy, ws, gw);
   } else if (b >= r0) {
     // the previous conv's weight-gradient slabs (another workspace), reduced here
     // instead of in a launch of their own
@@ -1405,8 +1409,30 @@ bool s2_ok(const Geom& g) {
   return g.stride == 2 && (g.RH & 1) == 0 && (g.RW & 1) == 0 && g.SH == g.RH / 2 && g.SW == g.RW / 2;
 }
 
+// Default split-K count of a FORWARD conv (data gradients keep one split, so the fused
+// backward launch and the separate data-gradient launch stay bit-identical): a function
+// of the geometry only (never of a tuned tile or
+// ring depth, so every tile / ring variant of a plan keeps one summation order).
+// Split-K pays where a long K loop runs on a grid of at most one 64x64 workgroup per
+// CU: layer4's 3x3 convs (72 K-steps, 200 tiles at batch 32: 23.2 -> 18.6 us forward,
+// 23.5 -> 18.6 us data gradient, graph-replayed) and its 2048->512 1x1 (32 K-steps:
+// 12.7 -> 11.9 us); fp32 the same shapes (32-channel K-steps): 90.1 -> 84.8, 43.7 -> 40.9
+// and 95.2 -> 83.7 us (profiles/r04_f32_conv_sweep.txt).  Everywhere else the merge (write-through partial stores, the
+// arrival atomic, the partial reads: ~3-5 us on the last arriver's critical path)
+// costs more than the shorter K loop saves (profiles/r04_splitk_sweep.txt).
+int default_splits(int dtype, int mode, const Geom& g, bool fused) {
+  if (fused || !(mode == kGemm || mode == kFwd || mode == kDgrad)) return 1;
+  (void)dtype;
+  const int ks = dtype == POSE6D_DT_BF16 ? 64 : 32;
+  const int nk = fast_nk(mode, g, ks);
+  const int64_t tiles64 = (int64_t)p6::ceil_div(g.M, 64) * p6::ceil_div(g.Ncols, 64);
+  if (nk >= 32 && tiles64 <= 256) return 2;
+  return 1;
+}
+
 // fused = the data-gradient half of conv_bwd_kernel (its workgroups are 64x64 / 4 waves)
-Plan choose(int dtype, int mode, const Geom& g, bool fused = false, const pose6d_tuning_t* tn = nullptr) {
+Plan choose(int dtype, int mode, const Geom& g, bool fused = false, const pose6d_tuning_t* tn = nullptr,
+            bool fwd = false) {
   Plan p{};
   p.fast = fast_ok(dtype, mode, g) && tune(tn, &pose6d_tuning_t::conv_base, 0) == 0;
   p.mode = mode;
@@ -1442,14 +1468,22 @@ Plan choose(int dtype, int mode, const Geom& g, bool fused = false, const pose6d
   if (p.stages > 6) p.stages = 6;
   if (p.stages == 5) p.stages = 4;
   if (cols128 && rows128 && p.stages > 4) p.stages = 4;   // 6 x 32 KiB exceeds the 160 KiB LDS
-  p.g.splits = tune(tn, &pose6d_tuning_t::conv_splitk, 1);
+  if (fused && p.stages == 3) p.stages = 4;   // the fused backward instantiates 2- and 4-slot data gradients
+  // data gradients split only where no fused backward exists for the conv (fp32 KxK: its
+  // weight gradient is register-staged), so fused == separate stays bit-exact elsewhere
+  const bool split_dgrad = dtype == POSE6D_DT_F32 && p.mode == kDgrad;
+  p.g.splits = tune(tn, &pose6d_tuning_t::conv_splitk,
+                    (fwd || split_dgrad) ? default_splits(dtype, p.mode, p.g, fused) : 1);
   if (fused || !(p.mode == kGemm || p.mode == kFwd || p.mode == kDgrad) || p.g.splits < 1) p.g.splits = 1;
+  // split-K plans keep their long-K ring depth (the sweep's fastest: 4 slots) unless tuned
+  if (p.g.splits > 1 && tune(tn, &pose6d_tuning_t::conv_stages, -1) < 0 && p.stages < 4 && !(cols128 && rows128))
+    p.stages = 4;
   return p;
 }
 
 int run_conv(int dtype, int mode, const Geom& g, const void* src, const void* w, const float* bias, const void* res,
-             void* out, float* stats, hipStream_t s, const pose6d_tuning_t* tn = nullptr) {
-  const Plan p = choose(dtype, mode, g, false, tn);
+             void* out, float* stats, hipStream_t s, const pose6d_tuning_t* tn = nullptr, bool fwd = false) {
+  const Plan p = choose(dtype, mode, g, false, tn, fwd);
   if (p.fast) return dispatch_fast(dtype, p.mode, p.g, p.tile, p.stages, src, w, bias, res, out, stats, s);
   return dtype == POSE6D_DT_BF16 ? dispatch<bf16>(mode, g, p.tile, src, w, bias, res, out, stats, s)
                                  : dispatch<float>(mode, g, p.tile, src, w, bias, res, out, stats, s);
@@ -1503,7 +1537,7 @@ extern "C" int pose6d_conv2d_fwd_tuned(int32_t dtype, const void* x, const void*
     P6_CHECK_ARG(g.log2SC >= 0 && Cin % bk == 0, "pose6d_conv2d_fwd: Cin must be 4 or a power of two >= %d (got %d)",
                  bk, Cin);
   if (mode == kGemm) P6_CHECK_ARG(Cin % bk == 0, "pose6d_conv2d_fwd: 1x1 Cin %% %d != 0", bk);
-  return run_conv(dtype, mode, g, x, w, bias, nullptr, y, stats, p6::stream_of(stream), tuning);
+  return run_conv(dtype, mode, g, x, w, bias, nullptr, y, stats, p6::stream_of(stream), tuning, true);
 }
 
 // eval-mode conv + BatchNorm apply (+ residual, + ReLU) in one launch: the store of
@@ -1532,7 +1566,7 @@ extern "C" int pose6d_conv2d_fwd_act(int32_t dtype, const void* x, const void* w
   g.act_shift = shift;
   g.act_rscale = res_scale;
   g.act_rshift = res_shift;
-  return run_conv(dtype, mode, g, x, w, bias, res, out, nullptr, p6::stream_of(stream));
+  return run_conv(dtype, mode, g, x, w, bias, res, out, nullptr, p6::stream_of(stream), nullptr, true);
 }
 
 extern "C" int pose6d_conv2d_fwd_act_dual(int32_t dtype, const void* x, const void* w, const void* xd, const void* wd,
@@ -1564,6 +1598,17 @@ extern "C" int pose6d_conv2d_fwd_act_dual(int32_t dtype, const void* x, const vo
   g.act_rshift = shift_d;
   const Plan p = choose(dtype, kGemmDual, g);
   P6_CHECK_ARG(p.fast, "pose6d_conv2d_fwd_act_dual: shape outside the LDS-DMA path");
+  // bit identity with the separate launches needs their K loops unsplit (the dual
+  // kernel has no split-K); pose6d_conv_variant reports the separate plans' splits
+  {
+    int m3, md;
+    const Geom g3 = fwd_geom(dtype, N, Ho, Wo, Cin, Cout, 1, 1, 1, 0, Ho, Wo, &m3);
+    const Geom gd = fwd_geom(dtype, N, Hd, Wd, Cind, Cout, 1, 1, stride_d, 0, Ho, Wo, &md);
+    P6_CHECK_ARG(choose(dtype, m3, g3, false, nullptr, true).g.splits == 1 &&
+                     choose(dtype, md, gd, false, nullptr, true).g.splits == 1,
+                 "pose6d_conv2d_fwd_act_dual: the separate launches of this pair split K (pose6d_conv_variant >> 16); "
+                 "run them separately");
+  }
   return dispatch_fast(dtype, kGemmDual, p.g, p.tile, p.stages, x, w, nullptr, nullptr, out, nullptr,
                        p6::stream_of(stream));
 }
@@ -1638,7 +1683,7 @@ extern "C" int pose6d_conv2d_dgrad_tuned(int32_t dtype, const void* dy, const vo
 
 namespace {
 
-template <int DMODE, int DS, int WS>
+template <int DMODE, int DS, int WS, typename T = bf16>
 int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void* wt, const void* dres, void* dx,
                const void* x, float* ws, const ReduceJob& rj, hipStream_t s) {
   Geom gd = gd0;
@@ -1648,10 +1693,10 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
   const int nd = gd.gm * gd.gn * (DMODE == kDgradS2 ? s2_classes(gd) : 1);
   const int nd_pad = (nd + 7) & ~7;
   const int nw = gw.gm * gw.gn * gw.splits;
-  const int nk = fast_nk(DMODE, gd);
+  const int nk = fast_nk(DMODE, gd, LK<T>::KS);
   const int ring_d = (nk < DS ? (nk > 0 ? nk : 1) : DS) * 128 * 128;
-  const int epi = 64 * (64 * 2 + 16) + (gd.bnr_part ? bnr_lds(4, 64) : 0);
-  const int ring_w = WS * 128 * 128;
+  const int epi = 64 * (64 * (int)sizeof(T) + 16) + (gd.bnr_part ? bnr_lds(4, 64) : 0);
+  const int ring_w = sizeof(T) == 2 ? WS * 128 * 128 : WS * WgF32<64>::STAGE;
   int lds = ring_d > epi ? ring_d : epi;
   lds = lds > ring_w ? lds : ring_w;
   // longest workgroups first: the weight gradient's K-steps per split against the
@@ -1661,16 +1706,18 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
 #endif
   const int wfirst = POSE6D_BWD_ORDER && p6::ceil_div(gw.mps, 64) >= nk;
   const int grid = wfirst ? ((nw + 7) & ~7) + nd + rj.nblk : nd_pad + nw + rj.nblk;
-  conv_bwd_kernel<DMODE, DS, WS><<<grid, kThreads, lds, s>>>(
-      (const bf16*)dy, (const bf16*)wt, (const bf16*)dres, (bf16*)dx, gd, nd, nd_pad, wfirst, (const bf16*)x, ws, gw,
-      rj);
+  conv_bwd_kernel<DMODE, DS, WS, T><<<grid, kThreads, lds, s>>>(
+      (const T*)dy, (const T*)wt, (const T*)dres, (T*)dx, gd, nd, nd_pad, wfirst, (const T*)x, ws, gw, rj);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }
 
 template <int DMODE>
-int launch_bwd_mode(int ds, const Geom& gd, const p6::WGeom& gw, const void* dy, const void* wt, const void* dres,
-                    void* dx, const void* x, float* ws, const ReduceJob& rj, hipStream_t s) {
+int launch_bwd_mode(int dtype, int ds, const Geom& gd, const p6::WGeom& gw, const void* dy, const void* wt,
+                    const void* dres, void* dx, const void* x, float* ws, const ReduceJob& rj, hipStream_t s) {
+  if (dtype == POSE6D_DT_F32)
+    return ds == 2 ? launch_bwd<DMODE, 2, POSE6D_WGRAD_STAGES_F32, float>(gd, gw, dy, wt, dres, dx, x, ws, rj, s)
+                   : launch_bwd<DMODE, 4, POSE6D_WGRAD_STAGES_F32, float>(gd, gw, dy, wt, dres, dx, x, ws, rj, s);
   return ds == 2 ? launch_bwd<DMODE, 2, POSE6D_WGRAD_STAGES>(gd, gw, dy, wt, dres, dx, x, ws, rj, s)
                  : launch_bwd<DMODE, 4, POSE6D_WGRAD_STAGES>(gd, gw, dy, wt, dres, dx, x, ws, rj, s);
 }
@@ -1683,9 +1730,10 @@ int launch_bwd_mode(int ds, const Geom& gd, const p6::WGeom& gw, const void* dy,
 // otherwise as the separate pose6d_conv2d_dgrad + pose6d_conv2d_wgrad launches.
 // dx == NULL: weight gradient only.
 namespace {
-bool bwd_fused(const Plan& pd, const p6::WgradPlan& pw, const pose6d_tuning_t* tn) {
-  return pd.fast && pd.tile == 3 && (pd.stages == 2 || pd.stages == 4) && pw.fast &&
-         pw.stages == POSE6D_WGRAD_STAGES &&
+bool bwd_fused(int dtype, const Plan& pd, const p6::WgradPlan& pw, const pose6d_tuning_t* tn) {
+  // the fused kernel carries the 64x64 weight-gradient bodies only
+  return pd.fast && pd.tile == 3 && (pd.stages == 2 || pd.stages == 4) && pw.fast && pw.bm == 64 &&
+         pw.stages == (dtype == POSE6D_DT_BF16 ? POSE6D_WGRAD_STAGES : POSE6D_WGRAD_STAGES_F32) &&
          tune(tn, &pose6d_tuning_t::bwd_separate, 0) == 0;
 }
 
@@ -1714,7 +1762,7 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
     if (!deferred || phases != 3) return POSE6D_OK;
     p6::WgradPlan pw;
     const p6::WGeom gw = p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw, tn);
-    if (pw.fast) return POSE6D_OK;
+    if (pw.fast && dtype == POSE6D_DT_BF16) return POSE6D_OK;   // bf16 LDS-DMA plans: the fused launch
     P6_CHECK_ARG((int64_t)pw.splits * Cout * gw.Kpad * 4 <= ws_bytes,
                  "pose6d_conv2d_backward: workspace %lld bytes < %lld needed", (long long)ws_bytes,
                  (long long)pw.splits * Cout * gw.Kpad * 4);
@@ -1743,10 +1791,10 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
   const Plan pd = choose(dtype, mode, gd0, true, tn);
   p6::WgradPlan pw;
   const p6::WGeom gw = p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw, tn);
-  const bool fused = bwd_fused(pd, pw, tn);
+  const bool fused = bwd_fused(dtype, pd, pw, tn);
   if (!fused) {
     if (!(phases & 1)) return POSE6D_OK;
-    const bool carry = deferred && phases == 3 && !pw.fast;
+    const bool carry = deferred && phases == 3 && (!pw.fast || dtype == POSE6D_DT_F32);
     int rc = carry ? POSE6D_OK : flush_prev();
     if (rc) return rc;
     rc = dgrad_impl(dtype, dy, wt, dres, dres_mask, dx, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, stream, tn,
@@ -1774,13 +1822,13 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
   if (phases & 1) {
     switch (pd.mode) {
       case kGemm:
-        rc = launch_bwd_mode<kGemm>(pd.stages, gd, gw, dy, wt, dres, dx, x, workspace, carried, s);
+        rc = launch_bwd_mode<kGemm>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, workspace, carried, s);
         break;
       case kDgradS2:
-        rc = launch_bwd_mode<kDgradS2>(pd.stages, gd, gw, dy, wt, dres, dx, x, workspace, carried, s);
+        rc = launch_bwd_mode<kDgradS2>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, workspace, carried, s);
         break;
       default:
-        rc = launch_bwd_mode<kDgrad>(pd.stages, gd, gw, dy, wt, dres, dx, x, workspace, carried, s);
+        rc = launch_bwd_mode<kDgrad>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, workspace, carried, s);
         break;
     }
   }
@@ -1830,8 +1878,8 @@ extern "C" int pose6d_conv_variant(int32_t dtype, int32_t pass, int32_t N, int32
   int mode;
   const Geom g = pass == 0 ? fwd_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode)
                            : dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
-  const Plan p = choose(dtype, mode, g);
-  return (p.stages << 12) | ((int)p.fast << 8) | (p.mode << 4) | p.tile;
+  const Plan p = choose(dtype, mode, g, false, nullptr, pass == 0);
+  return (p.g.splits << 16) | (p.stages << 12) | ((int)p.fast << 8) | (p.mode << 4) | p.tile;
 }
 
 // fused backward variant (profiling joins): (1 << 16) | (dgrad mode << 4) | data-gradient
@@ -1844,7 +1892,7 @@ extern "C" int pose6d_bwd_variant(int32_t dtype, int32_t N, int32_t H, int32_t W
   const Plan pd = choose(dtype, mode, gd0, true);
   p6::WgradPlan pw;
   p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
-  return bwd_fused(pd, pw, nullptr) ? (1 << 16) | (pd.mode << 4) | pd.stages : 0;
+  return bwd_fused(dtype, pd, pw, nullptr) ? (1 << 16) | (pd.mode << 4) | pd.stages : 0;
 }
 
 namespace {
@@ -1913,7 +1961,7 @@ extern "C" int pose6d_conv2d_backward_bn_rows(int32_t dtype, int32_t N, int32_t 
   const Plan pd = choose(dtype, mode, gd0, true);
   p6::WgradPlan pw;
   p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
-  return bnr_plan_rows(bwd_fused(pd, pw, nullptr) ? pd : choose(dtype, mode, gd0, false));
+  return bnr_plan_rows(bwd_fused(dtype, pd, pw, nullptr) ? pd : choose(dtype, mode, gd0, false));
 }
 
 extern "C" int pose6d_conv2d_backward_chain_bn(int32_t dtype, const void* x, const void* dy, const void* wt,

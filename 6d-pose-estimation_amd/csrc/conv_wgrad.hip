@@ -252,6 +252,45 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_lds_kernel(const bf16* __
   conv_wgrad_lds_body<64, 64, S, PW>(smem, blockIdx.x, x, dy, ws, g);
 }
 
+// fp32 LDS-DMA weight gradient (wgrad_body.h conv_wgrad_lds_body_f32); trailing
+// workgroups run a carried slab reduce of the previous conv (`rj`), as the
+// register-staged kernel does.  64x64 tiles take 64-pixel stages, 128x128 tiles
+// 32-pixel stages (32 KiB either way)
+template <int BT>
+constexpr int f32_ms() { return BT == 128 ? 32 : 64; }
+template <int S, bool PW, int BT>
+__global__ __launch_bounds__(kThreads) void conv_wgrad_lds_f32_kernel(const float* __restrict__ x,
+                                                                      const float* __restrict__ dy,
+                                                                      float* __restrict__ ws, WGeom g, ReduceJob rj) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tiles = g.gm * g.gn;
+  if ((int)blockIdx.x >= tiles * g.splits) {
+    run_reduce_job(smem, blockIdx.x - tiles * g.splits, rj);
+    return;
+  }
+  conv_wgrad_lds_body_f32<f32_ms<BT>(), S, PW, BT>(smem, blockIdx.x, x, dy, ws, g);
+}
+
+template <int S, int BT>
+int launch_fast_f32(const WGeom& g, const void* x, const void* dy, float* ws, hipStream_t s, const ReduceJob& rj) {
+  int lds = S * WgF32<f32_ms<BT>(), BT>::STAGE;
+  if (lds < acc_stage_bytes<BT, BT>()) lds = acc_stage_bytes<BT, BT>();
+  const int grid = g.gm * g.gn * g.splits + rj.nblk;
+  if (g.KH == 1 && g.KW == 1 && g.stride == 1 && g.pad == 0)
+    conv_wgrad_lds_f32_kernel<S, true, BT><<<grid, kThreads, lds, s>>>((const float*)x, (const float*)dy, ws, g, rj);
+  else
+    conv_wgrad_lds_f32_kernel<S, false, BT><<<grid, kThreads, lds, s>>>((const float*)x, (const float*)dy, ws, g, rj);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+int launch_fast_f32_any(const Plan& p, const WGeom& g, const void* x, const void* dy, float* ws, hipStream_t s,
+                        const ReduceJob& rj) {
+  if (p.bm == 128) return p.stages == 3 ? launch_fast_f32<3, 128>(g, x, dy, ws, s, rj)
+                                        : launch_fast_f32<2, 128>(g, x, dy, ws, s, rj);
+  return p.stages == 3 ? launch_fast_f32<3, 64>(g, x, dy, ws, s, rj) : launch_fast_f32<2, 64>(g, x, dy, ws, s, rj);
+}
+
 int tuned(const pose6d_tuning_t* t, int32_t pose6d_tuning_t::*f, int dflt) {
   return (t && t->*f >= 0) ? (int)(t->*f) : dflt;
 }
@@ -270,16 +309,49 @@ int tuned(const pose6d_tuning_t* t, int32_t pose6d_tuning_t::*f, int dflt) {
 #ifndef POSE6D_WGRAD_TARGET_F32
 #define POSE6D_WGRAD_TARGET_F32 512
 #endif
+#ifndef POSE6D_WGRAD_TARGET_F32_FAST
+#define POSE6D_WGRAD_TARGET_F32_FAST 512
+#endif
+
+
+#ifndef POSE6D_WGRAD_F32_KXK_BT
+#define POSE6D_WGRAD_F32_KXK_BT 128
+#endif
 
 // bf16 weight gradients take the LDS-DMA kernel (64x64 tiles, 3-slot ring) unless a
 // pose6d_tuning_t (tests / tools only) asks for the register-staged kernel or another ring
 Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* tn = nullptr) {
   Plan p{};
-  p.fast = dtype == POSE6D_DT_BF16 && SC % 64 == 0 && Cout % 64 == 0 &&
-           tuned(tn, &pose6d_tuning_t::wgrad_base, 0) == 0;
+  // wgrad_base: 0 = default, 1 = register-staged; fp32 only: 2 = LDS-DMA 64x64 tiles,
+  // 3 = LDS-DMA 128x128 tiles (each where the channel counts allow it, else the default)
+  const int wb = tuned(tn, &pose6d_tuning_t::wgrad_base, 0);
+  const bool ok64 = SC % 64 == 0 && Cout % 64 == 0, ok128 = SC % 128 == 0 && Cout % 128 == 0;
+  int f32_bt = 0;
+  if (dtype == POSE6D_DT_F32 && wb != 1) {
+    // default: 64x64 tiles for 1x1 filters and for Cout = 64, 128x128 for wider KxK
+    // convs (the 64x64 body lost to the register-staged 128x128 tile there: 28x28
+    // 128->128 3x3 85 vs 131 us, profiles/r04_f32_conv_sweep.txt)
+    if (wb == 2 && ok64) f32_bt = 64;
+    else if (wb == 3 && ok128) f32_bt = 128;
+    else if (ok64 && (Kpad == SC || Cout == 64)) f32_bt = 64;
+    else if (ok128) f32_bt = POSE6D_WGRAD_F32_KXK_BT;
+  }
+  p.fast = dtype == POSE6D_DT_F32 ? f32_bt != 0 : ok64 && wb == 0;
   int target, min_rows, step;
   int64_t max_bytes;
-  if (p.fast) {
+  if (p.fast && dtype == POSE6D_DT_F32) {
+    // fp32 LDS-DMA body: 32 KiB stages, 2 slots (two workgroups per CU), ~2
+    // workgroups per CU of splits
+    p.bm = f32_bt;
+    p.bn = f32_bt;
+    p.stages = tuned(tn, &pose6d_tuning_t::wgrad_stages, POSE6D_WGRAD_STAGES_F32);
+    if (p.stages < 2) p.stages = 2;
+    if (p.stages > 3) p.stages = 3;
+    target = POSE6D_WGRAD_TARGET_F32_FAST;
+    min_rows = 256;
+    step = f32_bt == 128 ? f32_ms<128>() : f32_ms<64>();
+    max_bytes = 64ll << 20;
+  } else if (p.fast) {
     p.bm = 64;
     p.bn = 64;
     p.stages = tuned(tn, &pose6d_tuning_t::wgrad_stages, POSE6D_WGRAD_STAGES);
@@ -402,7 +474,8 @@ int wgrad_reduce_launch(const float* ws, float* dw, int Cout, int Kpad, int SC, 
 
 int wgrad_launch_carry(int dtype, const WGeom& g, const WgradPlan& p, const void* x, const void* dy, float* ws,
                        const ReduceJob& rj, hipStream_t s) {
-  P6_CHECK_ARG(!p.fast, "wgrad_launch_carry: register-staged plans only");
+  P6_CHECK_ARG(!p.fast || dtype == POSE6D_DT_F32, "wgrad_launch_carry: register-staged or fp32 plans only");
+  if (p.fast) return launch_fast_f32_any(p, g, x, dy, ws, s, rj);
   return dtype == POSE6D_DT_BF16 ? launch_any<bf16>(g, p.bm, p.bn, x, dy, ws, s, rj)
                                  : launch_any<float>(g, p.bm, p.bn, x, dy, ws, s, rj);
 }
@@ -432,7 +505,9 @@ extern "C" int pose6d_conv2d_wgrad_tuned(int32_t dtype, const void* x, const voi
                "with the same tuning)", (long long)ws_bytes, (long long)p.splits * Cout * g.Kpad * 4);
   hipStream_t s = p6::stream_of(stream);
   int rc;
-  if (p.fast) {
+  if (p.fast && dtype == POSE6D_DT_F32) {
+    rc = launch_fast_f32_any(p, g, x, dy, workspace, s, ReduceJob{});
+  } else if (p.fast) {
     rc = p.stages == 2 ? launch_fast<2>(g, x, dy, workspace, s)
        : p.stages == 3 ? launch_fast<3>(g, x, dy, workspace, s)
                        : launch_fast<4>(g, x, dy, workspace, s);

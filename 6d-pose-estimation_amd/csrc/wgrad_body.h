@@ -10,6 +10,11 @@
 #ifndef POSE6D_WGRAD_STAGES
 #define POSE6D_WGRAD_STAGES 3
 #endif
+// LDS ring depth of the fp32 weight-gradient body (32 KiB stages): two slots keep two
+// workgroups per CU resident
+#ifndef POSE6D_WGRAD_STAGES_F32
+#define POSE6D_WGRAD_STAGES_F32 2
+#endif
 
 namespace p6 {
 
@@ -363,6 +368,190 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
   store_acc_tile<BM, BN, false>(acc, smem, slab + (int64_t)co0 * g.Kpad + k0, g.Kpad, BM, BN);
 }
 
+
+// ============================================================================
+// fp32 weight gradient on the LDS-DMA path (exact v_mfma_f32_16x16x4_f32): the
+// reference-precision training step's weight gradients (train_rgbd_geometric.py:106-112
+// trains in fp32).  64 (co) x 64 (k) tile on 4 waves (2 x 2, each 32 x 32 = 2 x 2
+// MFMA tiles); a stage is MS output pixels deep: dY [MS m][64 co] and X [MS m][64 k]
+// fp32 images, 256-byte rows, filled by LDS-DMA (one wave instruction = 4 rows), the
+// 16-byte chunk of odd rows XOR 4 (applied on the source address: the LDS side of
+// LDS-DMA is lane-linear).  The contraction runs over m, which is the ROW index of
+// both images, so an MFMA operand is one float per lane: A[i][k] = dY[m0 + k][co + i]
+// (lane i = l % 16, k = l / 16) -- four rows per 32-lane LDS group, conflict-free
+// under the swizzle (ds_read_b32 banks are (a / 4) mod 32).  The reads are inline asm
+// (hipcc would otherwise wait for the whole DMA ring before every LDS read), issued a
+// group of 4 m ahead of the MFMAs that consume them with counted lgkmcnt waits.
+// Replaces the register-staged conv_wgrad_kernel<float> (global loads -> VGPRs ->
+// ds_write -> __syncthreads per stage) on every fp32 conv with Cin, Cout multiples of 64.
+// ============================================================================
+template <int MS, int BT = 64>
+struct WgF32 {
+  static constexpr int ROWB = BT * 4;                // bytes per image row (BT fp32)
+  static constexpr int CPR = ROWB / 16;              // 16-byte chunks per row
+  static constexpr int RPI = 1024 / ROWB;            // rows per DMA wave instruction
+  static constexpr int IMG = MS * ROWB;              // bytes per image
+  static constexpr int STAGE = 2 * IMG;              // dY image, then X image
+  static constexpr int INS = MS / RPI;               // DMA instructions per image per stage
+  static constexpr int PER = INS / 4;                // ... per wave (4 waves)
+  static constexpr int LOADS = 2 * PER;              // DMA instructions per wave per stage
+  static constexpr int TT = BT / 32;                 // 16x16 MFMA tiles per wave and dimension
+  static_assert(BT == 64 || BT == 128, "BT: 64 or 128");
+  static_assert(PER * 4 == INS && MS % 16 == 0, "MS: a multiple of 16 pixels");
+};
+
+// the 8 operand reads (2 A + 2 B floats for each of two m-groups) of one MFMA group
+// pair, as one asm batch without a wait
+__device__ __forceinline__ void lds_read_b32x4(float (&f)[4], const unsigned (&a)[4]) {
+  asm volatile("ds_read_b32 %0, %4\n\tds_read_b32 %1, %5\n\tds_read_b32 %2, %6\n\tds_read_b32 %3, %7"
+               : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3])
+               : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]));
+}
+// wait until at most N LDS reads are outstanding; the operands of the group just
+// landed are redefined after the wait (no MFMA consuming them moves above it)
+template <int N>
+__device__ __forceinline__ void lds_wait_b32x4(float (&f)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]) : "n"(N));
+}
+
+template <int MS, int S, bool PW, int BT = 64>
+__device__ __forceinline__ void conv_wgrad_lds_body_f32(char* smem, int bid, const float* __restrict__ x,
+                                                        const float* __restrict__ dy, float* __restrict__ ws,
+                                                        const p6::WGeom& g) {
+  using C = WgF32<MS, BT>;
+  constexpr int PER = C::PER, LOADS = C::LOADS, STAGE = C::STAGE, IMG = C::IMG, TT = C::TT;
+  const int tiles = g.gm * g.gn;
+  const int nwg = tiles * g.splits;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int split = bid / tiles;   // all tiles of one pixel range share an XCD's L2
+  const int t2 = bid - split * tiles;
+  const int tm = t2 / g.gn, tn = t2 - tm * g.gn;
+  const int co0 = tm * BT, k0 = tn * BT;
+  const int mbeg = split * g.mps;
+  const int mend = min(g.M, mbeg + g.mps);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const char* zp = reinterpret_cast<const char*>(g_zero_page);
+  // the BT-wide k tile lies in one filter tap (SC % BT == 0)
+  const int tap = k0 >> g.log2SC, ci0 = k0 & (g.SC - 1);
+  const int tkh = tap / g.KW, tkw = tap - tkh * g.KW;
+  // DMA rows of this lane: instruction j (j = i * 4 + wave) covers rows RPI j .. RPI j +
+  // RPI - 1, the lane row RPI j + lane / CPR, chunk (lane % CPR) ^ (4 * odd row) of the row
+  const int rsub = lane / C::CPR;
+  const int ck = ((lane % C::CPR) ^ ((rsub & 1) << 2)) * 4;   // element offset of the fetched chunk
+  int rm[PER], rn[PER], roy[PER], rox[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int m = mbeg + C::RPI * (i * 4 + wave) + rsub;
+    rm[i] = m;
+    const int hw = g.RH * g.RW;
+    rn[i] = m / hw;
+    const int rem = m - rn[i] * hw;
+    roy[i] = rem / g.RW;
+    rox[i] = rem - roy[i] * g.RW;
+  }
+  const int step_y = MS / g.RW, step_x = MS - step_y * g.RW;
+  auto issue = [&](int buf) {
+    char* base = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int j = i * 4 + wave;
+      const bool ok = rm[i] < mend;
+      const void* py = ok ? (const void*)(dy + (int64_t)rm[i] * g.Cout + co0 + ck) : (const void*)zp;
+      glds16(py, base + j * 1024);
+      const void* px = zp;
+      if (PW) {
+        if (ok) px = x + ((int64_t)rm[i] << g.log2SC) + ci0 + ck;
+      } else {
+        const int yy = roy[i] * g.stride - g.pad + tkh, xx = rox[i] * g.stride - g.pad + tkw;
+        if (ok && (unsigned)yy < (unsigned)g.SH && (unsigned)xx < (unsigned)g.SW)
+          px = x + ((((int64_t)rn[i] * g.SH + yy) * g.SW + xx) << g.log2SC) + ci0 + ck;
+      }
+      glds16(px, base + IMG + j * 1024);
+      rm[i] += MS;
+      if (!PW) {
+        rox[i] += step_x;
+        roy[i] += step_y;
+        if (rox[i] >= g.RW) { rox[i] -= g.RW; ++roy[i]; }
+        while (roy[i] >= g.RH) { roy[i] -= g.RH; ++rn[i]; }
+      }
+    }
+  };
+
+  f32x4 acc[TT][TT];
+#pragma unroll
+  for (int i = 0; i < TT; ++i)
+#pragma unroll
+    for (int j = 0; j < TT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // operand addresses: m-group q (rows 4q .. 4q+3), lane row 4q + (lane >> 4), column c
+  // of the image at chunk (c >> 2) ^ (4 * odd row)
+  const int li = lane & 15, kq = lane >> 4;
+  // NB = 4-float read batches per group: TT A floats, then TT B floats
+  constexpr int NB = TT / 2;
+  unsigned off[2 * TT];
+#pragma unroll
+  for (int t = 0; t < TT; ++t) {
+    const int ca = wm * (BT / 2) + t * 16 + li, cb = wn * (BT / 2) + t * 16 + li;
+    off[t] = kq * C::ROWB + ((((ca >> 2) ^ ((kq & 1) << 2)) << 2) + (ca & 3)) * 4;
+    off[TT + t] = IMG + kq * C::ROWB + ((((cb >> 2) ^ ((kq & 1) << 2)) << 2) + (cb & 3)) * 4;
+  }
+  const unsigned ring = lds_addr(smem);
+  // one stage: MS / 4 m-groups of TT x TT MFMAs; operands of group q + 1 read while
+  // group q's MFMAs run (counted waits)
+  auto compute = [&](int buf, auto&& mid) {
+    const unsigned slot = ring + buf * STAGE;
+    constexpr int NQ = MS / 4;
+    // three register sets: a set is refilled two groups after its last use
+    float f[3][NB][4];
+    auto rd = [&](int q, float (&d)[NB][4]) {
+      const unsigned rq = slot + q * 4 * C::ROWB;
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const unsigned a[4] = {rq + off[4 * b], rq + off[4 * b + 1], rq + off[4 * b + 2], rq + off[4 * b + 3]};
+        lds_read_b32x4(d[b], a);
+      }
+    };
+    rd(0, f[0]);
+    mid();   // the next stage's DMA issue overlaps the first reads' latency
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      float (&cur)[NB][4] = f[q % 3];
+      if (q + 1 < NQ) {
+        rd(q + 1, f[(q + 1) % 3]);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) lds_wait_b32x4<4 * NB>(cur[b]);
+      } else {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) lds_wait_b32x4<0>(cur[b]);
+      }
+#pragma unroll
+      for (int i = 0; i < TT; ++i)
+#pragma unroll
+        for (int j = 0; j < TT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[i >> 2][i & 3], cur[(TT + j) >> 2][(TT + j) & 3],
+                                                          acc[i][j], 0, 0, 0);
+    }
+  };
+
+  const int nk = (mend - mbeg + MS - 1) / MS;
+  for (int s = 0; s < S - 1 && s < nk; ++s) issue(s);
+  int cur = 0, wbuf = S - 1;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int left = nk - 1 - kt;
+    wait_ahead<LOADS, S - 2>(left < S - 2 ? left : S - 2);
+    compute(cur, [&]() {
+      if (kt + S - 1 < nk) issue(wbuf);
+    });
+    cur = cur == S - 1 ? 0 : cur + 1;
+    wbuf = wbuf == S - 1 ? 0 : wbuf + 1;
+  }
+  asm volatile("s_barrier" ::: "memory");
+  float* slab = ws + (int64_t)split * g.Cout * g.Kpad;
+  store_acc_tile<BT, BT, false>(acc, smem, slab + (int64_t)co0 * g.Kpad + k0, g.Kpad, BT, BT);
+}
 
 // sum the split slabs (fixed order) into the OIHW fp32 gradient; k = (kh, kw, ci).
 // Block = L float4 lanes (4 consecutive k each) x G split groups: group g sums

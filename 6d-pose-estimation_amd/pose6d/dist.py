@@ -14,11 +14,14 @@ import torch
 import torch.distributed as dist
 
 
-def plan_buckets(sizes, bucket_elems):
+def plan_buckets(sizes, bucket_elems, tail_elems=0):
     """Bucket end offsets over a flat buffer holding tensors of `sizes` elements
     (with the given per-tensor offsets folded in by the caller): a bucket closes
     at the first tensor end that makes it >= bucket_elems; the last bucket ends
-    at the buffer end.  Returns [(tensor_index, end_offset)]."""
+    at the buffer end.  tail_elems > 0: a last bucket larger than that is split at
+    the tensor end that leaves the shortest suffix of at most tail_elems (or the last
+    tensor alone) -- the last bucket is only ready when the backward ends, so its
+    all-reduce is the step's unhidden tail.  Returns [(tensor_index, end_offset)]."""
     ends, start, off = [], 0, 0
     for i, (o, n) in enumerate(sizes):
         end = o + n
@@ -28,6 +31,21 @@ def plan_buckets(sizes, bucket_elems):
         off = end
     if sizes and (not ends or ends[-1][1] != off):
         ends.append((len(sizes) - 1, off))
+    if tail_elems > 0 and ends:
+        first = ends[-2][0] + 1 if len(ends) > 1 else 0   # the last bucket's first tensor
+        lo = ends[-2][1] if len(ends) > 1 else 0
+        if off - lo > tail_elems:
+            cut = None
+            for i in range(first, len(sizes) - 1):
+                e = sizes[i][0] + sizes[i][1]
+                if off - e <= tail_elems:
+                    cut = (i, e)
+                    break
+            if cut is None and len(sizes) - 1 > first:
+                i = len(sizes) - 2
+                cut = (i, sizes[i][0] + sizes[i][1])
+            if cut is not None:
+                ends.insert(len(ends) - 1, cut)
     return ends
 
 

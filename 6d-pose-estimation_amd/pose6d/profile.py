@@ -19,7 +19,7 @@ def _sym(v, T):
     bm, bn, nw = TILES[v & 15]
     mode = (v >> 4) & 15
     if (v >> 8) & 1:
-        return f"conv_lds_kernel<{T}, {bm}, {bn}, {mode}, {v >> 12}, false, {nw}>"
+        return f"conv_lds_kernel<{T}, {bm}, {bn}, {mode}, {(v >> 12) & 15}, false, {nw}>"
     return f"conv_igemm_kernel<{T}, {bm}, {bn}, {mode}, false>"
 
 
@@ -65,7 +65,10 @@ def conv_launches(eng, fused=True):
                      op.k, op.stride, op.pad, op.Ho, op.Wo, st)
             out.append((sym, flops, dgrad, op.name + ".dgrad"))
         v = query("wgrad_variant", dt, M, op.cout, op.k * op.k * op.cin_pad, op.cin_pad)
-        if (v >> 8) & 1:
+        if (v >> 8) & 1 and eng.dtype == torch.float32:
+            pw = str(op.k == 1 and op.stride == 1 and op.pad == 0).lower()
+            sym = f"conv_wgrad_lds_f32_kernel<{v >> 12}, {pw}, {128 if v & 2 else 64}>"
+        elif (v >> 8) & 1:
             sym = f"conv_wgrad_lds_kernel<64, 64, {v >> 12}>"
         else:
             sym = f"conv_wgrad_kernel<{T}, {128 if v & 2 else 64}, {128 if v & 1 else 64}>"

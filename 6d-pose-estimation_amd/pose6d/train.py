@@ -71,7 +71,7 @@ class RGBDGeometricTrainer:
 
     def __init__(self, model, batch, dtype=torch.bfloat16, lr=1e-4, weight_decay=1e-4, max_norm=1.0,
                  betas=(0.9, 0.999), eps=1e-8, rot_weight=1.0, trans_weight=10.0, process_group=None,
-                 bucket_mb=25.0):
+                 bucket_mb=25.0, tail_mb=2.0):
         self.model = model
         self.B = batch
         dev = next(model.parameters()).device
@@ -113,17 +113,19 @@ class RGBDGeometricTrainer:
         self.wr, self.wt = float(rot_weight), float(trans_weight)
         self.pg = process_group
         self.graphs = None
-        self._buckets(bucket_mb)
+        self._buckets(bucket_mb, tail_mb)
 
     # ------------------------------------------------------------- DDP buckets
-    def _buckets(self, bucket_mb):
+    def _buckets(self, bucket_mb, tail_mb=0.0):
         """Split the flat gradient into contiguous buckets; each closes after the
-        backward of the conv whose weight is its last parameter."""
+        backward of the conv whose weight is its last parameter.  The last bucket
+        (stem / layer1, ready only when the backward ends: its all-reduce is not
+        overlapped) is capped at tail_mb (tools/ddp_overlap.py models the tail)."""
         self.bucket_ends = []
         if self.world == 1:
             return
         sizes = [(off, p.numel()) for p, off in zip(self.arena.params, self.arena.offsets)]
-        ends = plan_buckets(sizes, int(bucket_mb * 1e6 / 4))
+        ends = plan_buckets(sizes, int(bucket_mb * 1e6 / 4), int(tail_mb * 1e6 / 4))
         ends[-1] = (ends[-1][0], self.arena.numel)   # the last bucket covers the alignment tail
         self.bucket_ends = [(self.arena.params[i], e) for i, e in ends]
 

@@ -41,6 +41,21 @@ class _BnReduce(ctypes.Structure):
         ("rows", ctypes.c_int32)]
 
 
+class _BnStats(ctypes.Structure):
+    """pose6d_bn_stats_t (include/pose6d.h): one BN of pose6d_bn_finalize_dual."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("partial", "gamma", "beta", "running_mean", "running_var",
+                                                "num_batches", "scale", "shift", "save_mean", "save_invstd")] + [
+        ("momentum", ctypes.c_float), ("eps", ctypes.c_float), ("C", ctypes.c_int32)]
+
+
+def _bn_stats(op):
+    bn = op.bn
+    p = [op.stats, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked, op.scale, op.shift,
+         op.mean, op.inv]
+    return _BnStats(*[t.data_ptr() if t is not None else None for t in p],
+                    float(bn.momentum if bn.momentum is not None else 0.1), float(bn.eps), op.cout)
+
+
 # pose6d_bn_fold_t (include/pose6d.h): eval-mode BN fold table entry
 _FOLD = np.dtype([("gamma", "<u8"), ("beta", "<u8"), ("rmean", "<u8"), ("rvar", "<u8"), ("scale", "<u8"),
                   ("shift", "<u8"), ("smean", "<u8"), ("sinv", "<u8"), ("eps", "<f4"), ("C", "<i4")])
@@ -359,6 +374,18 @@ class TrunkEngine:
         if fold:
             self._eval_fold(st)
             dual = self._dual_pairs()
+        # training: a downsampling block's two BN finalizes (bn3, downsample BN: same
+        # output grid) as one launch after conv3 (pose6d_bn_finalize_dual)
+        fin2 = {}
+        if training and not fold and self.bn_dual_finalize:
+            pos = {id(o): i for i, o in enumerate(self.ops)}
+            for op in self.ops:
+                if isinstance(op, _ActOp) and op.res_conv is not None:
+                    c3, r = op.cop, op.res_conv
+                    if (pos[id(r)] < pos[id(c3)] and c3.stats_rows == r.stats_rows
+                            and (c3.Ho, c3.Wo) == (r.Ho, r.Wo)):
+                        fin2[c3] = r
+                        fin2[r] = None
         for op in self.ops:
             if isinstance(op, _ConvOp):
                 if op in dual:
@@ -390,7 +417,15 @@ class TrunkEngine:
                     continue
                 call("conv2d_fwd", dt, op.src.t, op.wp, bias, op.out.t, op.stats if training else None, B, op.H,
                      op.W, op.cin_pad, op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, st)
-                if not fold:
+                if fold:
+                    pass
+                elif op in fin2:
+                    r = fin2[op]
+                    if r is not None:   # conv3: both BNs now; the downsample BN's finalize waited for it
+                        a, b = _bn_stats(op), _bn_stats(r)
+                        call("bn_finalize_dual", ctypes.addressof(a), ctypes.addressof(b), op.stats_rows,
+                             B * op.Ho * op.Wo, st)
+                else:
                     call(*fin)
             elif isinstance(op, _ActOp):
                 if op.pooled or fold:
@@ -444,6 +479,10 @@ class TrunkEngine:
                   and c3.conv.bias is None and r.conv.bias is None
                   and c3.cin_pad % ks == 0 and r.cin_pad % ks == 0 and c3.cout == r.cout
                   and (r.Ho, r.Wo) == (c3.Ho, c3.Wo) and self.B * c3.Ho * c3.Wo >= min_rows)
+            # the dual kernel has no split-K: a pair whose separate launches split K
+            # (small grids, long K) stays separate, so both paths agree bit for bit
+            ok = ok and all(query("conv_variant", self.dt, 0, self.B, c.H, c.W, c.cin_pad, c.cout, 1, 1, c.stride, 0,
+                                  c.Ho, c.Wo) >> 16 == 1 for c in (c3, r))
             if ok:
                 pairs[c3] = r
                 pairs[r] = None
@@ -605,6 +644,9 @@ class TrunkEngine:
     # training backward: a downsampling block's two BatchNorm backwards in one set of
     # launches (bit-identical to two pose6d_bn_bwd_mask calls; attribute for the tests)
     bwd_dual_bn = True
+    # training forward: a downsampling block's two BN finalizes in one launch
+    # (bit-identical to two pose6d_bn_finalize calls; attribute for the tests)
+    bn_dual_finalize = True
     # training backward: a BN + ReLU whose output gradient one data-gradient launch
     # completes gets its reduce pass from that launch's epilogue (attribute for the tests)
     bwd_conv_bn_reduce = True

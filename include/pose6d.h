@@ -188,10 +188,11 @@ int pose6d_conv2d_fwd(int32_t dtype, const void *x, const void *wp, const float 
                       int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW,
                       int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, void *stream);
 /* kernel variant a conv launch selects (profiling joins): fwd/dgrad (pass 0/1):
- * (stages << 12) | (fast << 8) | (mode << 4) | tile (tile 0..3 = 128x128, 128x64,
+ * (splits << 16) | (stages << 12) | (fast << 8) | (mode << 4) | tile (tile 0..3 = 128x128, 128x64,
  * 64x128, 64x64; mode 0 gemm, 1 im2col, 2 narrow stem, 3 dgrad, 4 stride-2 dgrad
  * split into output parity classes; fast = LDS-DMA bf16 kernel with an LDS ring
- * of `stages` K-steps, 0 on the register-staged kernel);
+ * of `stages` K-steps, 0 on the register-staged kernel; splits = workgroups per output
+ * tile of the in-launch split-K, 1 = none);
  * wgrad (pose6d_wgrad_variant, Cin = the padded channel count): (stages << 12) |
  * (fast << 8) | (BM == 128) << 1 | (BN == 128); fast = LDS-DMA 64x64 kernel. */
 int pose6d_conv_variant(int32_t dtype, int32_t pass, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout,
@@ -211,7 +212,8 @@ int pose6d_conv2d_fwd_act(int32_t dtype, const void *x, const void *w, const flo
  * x [N][Ho][Wo][Cin] (conv3 input), w [Cout][Cin]; xd [N][Hd][Wd][Cind] (block input),
  * wd [Cout][Cind], xd_s = xd sampled every stride_d pixels; both 1x1, no bias.  Bit for
  * bit pose6d_conv2d_fwd of the downsample then pose6d_conv2d_fwd_act with
- * res_scale/res_shift, without the downsample output's HBM round trip. */
+ * res_scale/res_shift, without the downsample output's HBM round trip.  Rejected
+ * (POSE6D_ERR_ARG) when either separate launch's plan splits K (pose6d_conv_variant). */
 int pose6d_conv2d_fwd_act_dual(int32_t dtype, const void *x, const void *w, const void *xd, const void *wd, void *out,
                                int32_t N, int32_t Ho, int32_t Wo, int32_t Cin, int32_t Cout, int32_t Hd, int32_t Wd,
                                int32_t Cind, int32_t stride_d, const float *scale, const float *shift,
@@ -362,6 +364,20 @@ int pose6d_bn_finalize(const float *partial, int32_t rows, int32_t C, int64_t co
                        const float *beta, float *running_mean, float *running_var, int64_t *num_batches,
                        float momentum, float eps, int32_t training, float *scale, float *shift, float *save_mean,
                        float *save_invstd, double *workspace, void *stream);
+/* pose6d_bn_finalize (training) of two BatchNorms over the same output grid -- a
+ * downsampling Bottleneck's bn3 and its downsample BN (same rows, count) -- in ONE
+ * launch; each BN's results bit for bit those of its own pose6d_bn_finalize call. */
+typedef struct {
+  const float *partial;   /* [2][C][rows] conv-epilogue statistics */
+  const float *gamma, *beta;
+  float *running_mean, *running_var;
+  int64_t *num_batches;   /* may be NULL */
+  float *scale, *shift, *save_mean, *save_invstd;
+  float momentum, eps;
+  int32_t C;
+} pose6d_bn_stats_t;
+int pose6d_bn_finalize_dual(const pose6d_bn_stats_t *a, const pose6d_bn_stats_t *b, int32_t rows, int64_t count,
+                            void *stream);
 /* Eval-mode fold of a table of BatchNorms in one launch: per entry and channel c,
  * scale = gamma / sqrt(running_var + eps), shift = beta - running_mean * scale,
  * save_mean = running_mean, save_invstd = 1 / sqrt(running_var + eps) -- pose6d_bn_finalize

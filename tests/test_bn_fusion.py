@@ -105,6 +105,36 @@ def test_trunk_backward_dual_bn_is_bit_identical(dtype):
         assert torch.equal(grads[0][p], grads[1][p])
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_trunk_forward_dual_bn_finalize_is_bit_identical(dtype):
+    """Training trunk forward with each downsampling block's bn3 + downsample-BN
+    finalize as ONE launch (pose6d_bn_finalize_dual) equals the two-call path bit for
+    bit: features, running statistics, num_batches_tracked, saved mean / invstd."""
+    from pose6d.resnet import resnet50_trunk
+    from pose6d.trunk import TrunkEngine
+    torch.manual_seed(0)
+    seq = resnet50_trunk(3).cuda().train()
+    eng = TrunkEngine(seq, 3)
+    eng.set_dtype(dtype)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(4, 3, 96, 96, generator=g).cuda()
+    init = {k: v.clone() for k, v in seq.state_dict().items()}
+    res = []
+    for dual in (False, True):
+        seq.load_state_dict(init)
+        eng.bn_dual_finalize = dual
+        feat = eng.forward(x, True).clone()
+        saved = [t.clone() for op in eng.convs for t in (op.mean, op.inv, op.scale, op.shift)]
+        torch.cuda.synchronize()
+        res.append((feat, {k: v.clone() for k, v in seq.state_dict().items()}, saved))
+    assert torch.equal(res[0][0], res[1][0])
+    for k in init:
+        assert torch.equal(res[0][1][k], res[1][1][k]), k
+    assert int(res[1][1]["4.0.downsample.1.num_batches_tracked"]) == 1
+    for a, b in zip(res[0][2], res[1][2]):
+        assert torch.equal(a, b)
+
+
 def _nhwc(t):
     return t.permute(0, 2, 3, 1).contiguous()
 

@@ -484,16 +484,18 @@ def test_backward_chain_carried_reduce(dtype):
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_wgrad_fast_vs_register_staged(dtype):
-    """The LDS-DMA weight gradient (bf16 and, since round 4, fp32) against the
-    register-staged kernel (Tuning(wgrad_base=1)) and the torch op: other split plans
-    sum the pixels in another order, so close, not equal; a stride-2 3x3, a partial
-    last split and a 1x1 with more than one k tile."""
+    """The LDS-DMA weight gradient (bf16 and, since round 4, fp32 with 64x64 and 128x128
+    tiles: Tuning(wgrad_base=2 / 3)) against the register-staged kernel
+    (Tuning(wgrad_base=1)) and the torch op: other split plans sum the pixels in another
+    order, so close, not equal; a stride-2 3x3, a partial last split and a 1x1 with more
+    than one k tile."""
     from pose6d._lib import Tuning, call, query, stream
     from pose6d.trunk import DTYPES
     g = torch.Generator().manual_seed(5)
     dev, dt = "cuda", DTYPES[dtype]
     for (N, H, W, Cin, Cout, k, s, p) in [(2, 28, 28, 128, 128, 3, 2, 1), (3, 15, 15, 64, 128, 3, 1, 1),
-                                          (2, 14, 14, 256, 192, 1, 1, 0), (2, 28, 28, 64, 256, 1, 2, 0)]:
+                                          (2, 14, 14, 256, 192, 1, 1, 0), (2, 28, 28, 64, 256, 1, 2, 0),
+                                          (3, 9, 9, 256, 256, 3, 1, 1), (2, 13, 13, 128, 256, 1, 1, 0)]:
         Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         x = torch.randn(N, Cin, H, W, generator=g)
         dyt = torch.randn(N, Cout, Ho, Wo, generator=g)
@@ -502,7 +504,10 @@ def test_wgrad_fast_vs_register_staged(dtype):
         ref = torch.nn.grad.conv2d_weight(x.double(), (Cout, Cin, k, k), dyt.double(), stride=s, padding=p)
         xd, dyd = _nhwc(x).to(dev, dtype), _nhwc(dyt).to(dev, dtype)
         outs = []
-        for tn in (Tuning(), Tuning(wgrad_base=1)):
+        tunings = [Tuning(), Tuning(wgrad_base=1)]
+        if dtype == torch.float32:
+            tunings += [Tuning(wgrad_base=2), Tuning(wgrad_base=3)]
+        for tn in tunings:
             ws = torch.empty(query("conv2d_wgrad_workspace_tuned", dt, N, Ho, Wo, Cin, Cout, k, k, tn.ref) // 4 + 1,
                              device=dev)
             dw = torch.empty(Cout, Cin, k, k, device=dev)
@@ -510,8 +515,8 @@ def test_wgrad_fast_vs_register_staged(dtype):
                  Ho, Wo, tn.ref, stream())
             torch.cuda.synchronize()
             outs.append(dw.cpu())
-        _close(outs[0], ref.float(), 1e-4, f"wgrad fast {(H, Cin, Cout, k, s)}")
-        _close(outs[1], ref.float(), 1e-4, f"wgrad base {(H, Cin, Cout, k, s)}")
+        for i, o in enumerate(outs):   # default, register-staged, [fp32 64x64, 128x128]
+            _close(o, ref.float(), 1e-4, f"wgrad plan {i} {(H, Cin, Cout, k, s)}")
 
 
 @pytest.mark.gpu

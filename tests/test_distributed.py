@@ -49,6 +49,34 @@ def test_plan_buckets_covers_arena():
         assert x == sizes[i][0] + sizes[i][1]                            # buckets close at tensor ends
 
 
+@pytest.mark.parametrize("tail", [50_000, 300_000, 900_000])
+def test_plan_buckets_tail_cap(tail):
+    """tail_elems: the last bucket is split at a tensor end so that it holds at most
+    `tail` elements (or only the last tensor); the other buckets are unchanged."""
+    from pose6d.dist import plan_buckets
+    rng = np.random.default_rng(1)
+    sizes, off = [], 0
+    for _ in range(120):
+        n = int(rng.integers(1, 200_000))
+        sizes.append((off, n))
+        off += n
+    base = plan_buckets(sizes, 2_500_000)
+    ends = plan_buckets(sizes, 2_500_000, tail)
+    e = [x for _, x in ends]
+    assert e == sorted(e) and len(set(e)) == len(e) and e[-1] == off
+    for i, x in ends:
+        assert x == sizes[i][0] + sizes[i][1]
+    lo = base[-2][1] if len(base) > 1 else 0
+    if off - lo > tail:
+        assert ends[:-2] == base[:-1] and len(ends) == len(base) + 1
+        assert off - e[-2] <= tail or e[-2] == sizes[-2][0] + sizes[-2][1]
+        # the shortest suffix within the cap: one tensor more would exceed it
+        k = [i for i, _ in ends][-2]
+        assert off - (sizes[k][0]) > tail or k == [i for i, _ in base][-2] + 1
+    else:
+        assert ends == base
+
+
 def _reducer_worker(rank, n, ends):
     from pose6d.dist import BucketReducer
     g = torch.arange(n, dtype=torch.float32) * (rank + 1)

@@ -90,7 +90,9 @@ def test_eval_downsample_in_block_launch_is_bit_identical(dtype):
         with torch.no_grad():
             feats.append(eng.forward(x, False).clone())
         torch.cuda.synchronize()
-    assert len(eng._dual_pairs()) == 8   # 4 blocks x (conv3, downsample)
+    # 4 blocks x (conv3, downsample); fp32 layer4's downsample (K = 1024 on a
+    # 128-tile grid) splits K in its own launch, so that pair stays separate
+    assert len(eng._dual_pairs()) == (6 if dtype == torch.float32 else 8)
     assert torch.equal(feats[0], feats[1])
 
 

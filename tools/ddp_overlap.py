@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--tail-mb", default="0,2,4,8", help="last-bucket caps to model (0 = none; the trainer's "
+                                                        "default is 2)")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--out", default="")
     a = ap.parse_args()
@@ -47,9 +49,11 @@ def main():
     data = synth_batch(a.batch, dev, seed=1000)
     # the DDP trainer's buckets (train.py: plan_buckets over the arena in gradient order)
     sizes = [(off, p.numel()) for p, off in zip(tr.arena.params, tr.arena.offsets)]
-    ends = plan_buckets(sizes, int(a.bucket_mb * 1e6 / 4))
-    ends[-1] = (ends[-1][0], tr.arena.numel)
-    bucket_ends = [e for _, e in ends]
+    plans = {}
+    for t in [float(v) for v in a.tail_mb.split(",")]:
+        ends = plan_buckets(sizes, int(a.bucket_mb * 1e6 / 4), int(t * 1e6 / 4))
+        ends[-1] = (ends[-1][0], tr.arena.numel)
+        plans[f"tail{t:g}MB"] = [e for _, e in ends]
 
     tr.capture(data)
     for _ in range(3):
@@ -107,39 +111,45 @@ def main():
     step_us = cum[-1]
     bwd_start_us = cum[state["bwd_start"]]
     bwd_end_us = cum[state["bwd_end"]]
-    # ready time of each bucket: the first mark whose prefix covers the bucket end
-    ready = []
-    for be in bucket_ends:
-        t = None
-        for nodes, upto in marks:
-            if upto >= be:
-                t = cum[min(nodes, n_nodes)]
-                break
-        ready.append(bwd_end_us if t is None else t)
-    sizes_b = [4 * (e - s) for s, e in zip([0] + bucket_ends[:-1], bucket_ends)]
-    scen = {}
-    for N in (2, 4, 8):
-        for name, busbw, alpha in (("one_link_153GBps", 153e9, 30.0), ("rccl_300GBps", 300e9, 30.0),
-                                   ("rccl_500GBps", 500e9, 30.0)):
-            t_end = 0.0
-            starts = []
-            for r, b in zip(ready, sizes_b):
-                t0 = max(r, t_end)
-                dur = alpha + 2 * (N - 1) / N * b / busbw * 1e6
-                t_end = t0 + dur
-                starts.append((round(t0, 1), round(dur, 1)))
-            tail = max(0.0, t_end - bwd_end_us)
-            scen[f"N{N}_{name}"] = {"tail_us": round(tail, 1), "comm_total_us": round(sum(d for _, d in starts), 1),
-                                    "predicted_efficiency": round(step_us / (step_us + tail), 4),
-                                    "buckets_start_dur_us": starts}
+
+    def model(bucket_ends):
+        # ready time of each bucket: the first mark whose prefix covers the bucket end
+        ready = []
+        for be in bucket_ends:
+            t = None
+            for nodes, upto in marks:
+                if upto >= be:
+                    t = cum[min(nodes, n_nodes)]
+                    break
+            ready.append(bwd_end_us if t is None else t)
+        sizes_b = [4 * (e - s) for s, e in zip([0] + bucket_ends[:-1], bucket_ends)]
+        scen = {}
+        for N in (2, 4, 8):
+            for name, busbw, alpha in (("one_link_153GBps", 153e9, 30.0), ("rccl_300GBps", 300e9, 30.0),
+                                       ("rccl_500GBps", 500e9, 30.0)):
+                t_end = 0.0
+                starts = []
+                for r, b in zip(ready, sizes_b):
+                    t0 = max(r, t_end)
+                    dur = alpha + 2 * (N - 1) / N * b / busbw * 1e6
+                    t_end = t0 + dur
+                    starts.append((round(t0, 1), round(dur, 1)))
+                tail = max(0.0, t_end - bwd_end_us)
+                scen[f"N{N}_{name}"] = {"tail_us": round(tail, 1),
+                                        "comm_total_us": round(sum(d for _, d in starts), 1),
+                                        "predicted_efficiency": round(step_us / (step_us + tail), 4),
+                                        "buckets_start_dur_us": starts}
+        return {"buckets": [{"bytes": b, "ready_us": round(r, 1)} for b, r in zip(sizes_b, ready)],
+                "scenarios": scen}
+
     res = {"dtype": a.dtype, "batch_per_rank": a.batch, "bucket_mb": a.bucket_mb, "step_ms_plain": round(step_ms, 4),
            "step_us_instrumented_sum": round(step_us, 1), "backward_start_us": round(bwd_start_us, 1),
            "backward_end_us": round(bwd_end_us, 1), "gradient_bytes": 4 * tr.arena.numel,
-           "buckets": [{"bytes": b, "ready_us": round(r, 1)} for b, r in zip(sizes_b, ready)],
            "model": "comm stream replays buckets in order: start = max(ready, previous end), duration = alpha + "
                     "2(N-1)/N * bytes / busbw; tail = comm end - backward end; efficiency = step / (step + tail); "
-                    "UNMEASURED on hardware (no multi-GPU node); RCCL's compute interference not modelled",
-           "scenarios": scen}
+                    "UNMEASURED on hardware (no multi-GPU node); RCCL's compute interference not modelled; "
+                    "plans: the 25 MB greedy buckets with the last bucket capped at tail MB (trainer default 2)",
+           "plans": {k: model(v) for k, v in plans.items()}}
     print(json.dumps(res, indent=1))
     if a.out:
         with open(a.out, "w") as f:

@@ -1,12 +1,12 @@
 #!/bin/bash
 # PMC counter passes over tools/conv_bench.py for ONE conv shape and pass
 # (one counter group per rocprofv3 run; kernel trace for durations).
-# usage: tools/pmc_one.sh TAG SHAPE_INDEX PASS
-TAG=$1; IDX=$2; PASS=$3
+# usage: tools/pmc_one.sh TAG SHAPE_INDEX PASS [bf16|f32]
+TAG=$1; IDX=$2; PASS=$3; DT=${4:-bf16}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc1_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-B="$GRAFT_REPO_ROOT/tools/conv_bench.py --only $IDX --passes $PASS --impls fast --tiles auto"
+B="$GRAFT_REPO_ROOT/tools/conv_bench.py --only $IDX --passes $PASS --impls fast --tiles auto --dtype $DT"
 i=0
 for G in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS" \
          "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM SQ_INSTS_LDS SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS" \
