@@ -62,11 +62,16 @@ def load():
                           " or `make -C 6d-pose-estimation_amd/csrc`")
     lib = ctypes.CDLL(LIB_PATH)
     protos = _parse_header(HEADER) if os.path.exists(HEADER) else {}
+    missing = []
     for name, (argtypes, ret) in protos.items():
+        if not hasattr(lib, name):   # a header newer than the build: fails when called
+            missing.append(name)
+            continue
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = {"int": ctypes.c_int, "int64_t": ctypes.c_int64}.get(ret, ctypes.c_char_p)
     lib._protos = protos
+    lib._missing = missing
     _lib = lib
     return lib
 
@@ -102,6 +107,9 @@ def query(name, *args):
 def call(name, *args):
     """Call pose6d_<name>; tensors are passed as data pointers; raise on error."""
     lib = load()
+    if "pose6d_" + name in lib._missing:
+        raise Pose6dError(f"pose6d_{name} is declared in include/pose6d.h but missing from {LIB_PATH} "
+                          "(stale build: rebuild the library)")
     fn = getattr(lib, "pose6d_" + name)
     conv = []
     for a in args:
