@@ -255,7 +255,12 @@ int pose6d_conv2d_backward(int32_t dtype, const void *x, const void *dy, const v
  *   wgrad_base    1: the register-staged weight-gradient kernel (other split plan)
  *   bwd_separate  1: data and weight gradient as separate launches (not the fused kernel)
  *   conv_splitk   fast path (1x1 / KxK forward, stride-1 data gradient): K-steps of each output tile
- *                 split over this many workgroups of one launch (1 = none) */
+ *                 split over this many workgroups of one launch (1 = none)
+ * Split-K plans (the default for long-K convs on small grids, see pose6d_conv_variant
+ * >> 16) keep their partial tiles and arrival counters in ONE library-owned device
+ * buffer: conv launches on different streams must not run concurrently unless all but
+ * one of them pass conv_splitk = 1 (stream-ordered use, e.g. one compute stream per
+ * process as the trainer and the DDP path have, is always safe). */
 typedef struct {
   int32_t conv_tile, conv_stages, conv_s2, conv_base, wgrad_stages, wgrad_base, bwd_separate, conv_splitk;
 } pose6d_tuning_t;
