@@ -1685,7 +1685,7 @@ namespace {
 
 template <int DMODE, int DS, int WS, typename T = bf16>
 int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void* wt, const void* dres, void* dx,
-               const void* x, float* ws, const ReduceJob& rj, hipStream_t s) {
+               const void* x, float* ws, const ReduceJob& rj, hipStream_t s, int order) {
   Geom gd = gd0;
   gd.gm = p6::ceil_div(gd.M, 64);
   gd.gn = p6::ceil_div(gd.Ncols, 64);
@@ -1700,11 +1700,17 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
   int lds = ring_d > epi ? ring_d : epi;
   lds = lds > ring_w ? lds : ring_w;
   // longest workgroups first: the weight gradient's K-steps per split against the
-  // data gradient's K-steps per tile
+  // data gradient's K-steps per tile.  fp32: a 64-pixel weight-gradient stage is twice
+  // the MACs of a 32-channel data-gradient K-step (28x28 128->512 fp32: 79.5 -> 72.5 us
+  // with the weight gradient first, profiles/r04_bwd_plan_sweep.txt)
+#ifndef POSE6D_BWD_WSTEP_F32
+#define POSE6D_BWD_WSTEP_F32 2   // build-time (A/B): 1 = compare stages and K-steps 1:1 for fp32 too
+#endif
+  constexpr int WSTEP = sizeof(T) == 4 ? POSE6D_BWD_WSTEP_F32 : 1;
 #ifndef POSE6D_BWD_ORDER
 #define POSE6D_BWD_ORDER 1   // build-time (A/B): 0 = the data gradient always first
 #endif
-  const int wfirst = POSE6D_BWD_ORDER && p6::ceil_div(gw.mps, 64) >= nk;
+  const int wfirst = order >= 0 ? order : (POSE6D_BWD_ORDER && WSTEP * p6::ceil_div(gw.mps, 64) >= nk);
   const int grid = wfirst ? ((nw + 7) & ~7) + nd + rj.nblk : nd_pad + nw + rj.nblk;
   conv_bwd_kernel<DMODE, DS, WS, T><<<grid, kThreads, lds, s>>>(
       (const T*)dy, (const T*)wt, (const T*)dres, (T*)dx, gd, nd, nd_pad, wfirst, (const T*)x, ws, gw, rj);
@@ -1714,12 +1720,14 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
 
 template <int DMODE>
 int launch_bwd_mode(int dtype, int ds, const Geom& gd, const p6::WGeom& gw, const void* dy, const void* wt,
-                    const void* dres, void* dx, const void* x, float* ws, const ReduceJob& rj, hipStream_t s) {
+                    const void* dres, void* dx, const void* x, float* ws, const ReduceJob& rj, hipStream_t s,
+                    int order) {
   if (dtype == POSE6D_DT_F32)
-    return ds == 2 ? launch_bwd<DMODE, 2, POSE6D_WGRAD_STAGES_F32, float>(gd, gw, dy, wt, dres, dx, x, ws, rj, s)
-                   : launch_bwd<DMODE, 4, POSE6D_WGRAD_STAGES_F32, float>(gd, gw, dy, wt, dres, dx, x, ws, rj, s);
-  return ds == 2 ? launch_bwd<DMODE, 2, POSE6D_WGRAD_STAGES>(gd, gw, dy, wt, dres, dx, x, ws, rj, s)
-                 : launch_bwd<DMODE, 4, POSE6D_WGRAD_STAGES>(gd, gw, dy, wt, dres, dx, x, ws, rj, s);
+    return ds == 2 ? launch_bwd<DMODE, 2, POSE6D_WGRAD_STAGES_F32, float>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order)
+                   : launch_bwd<DMODE, 4, POSE6D_WGRAD_STAGES_F32, float>(gd, gw, dy, wt, dres, dx, x, ws, rj, s,
+                                                                           order);
+  return ds == 2 ? launch_bwd<DMODE, 2, POSE6D_WGRAD_STAGES>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order)
+                 : launch_bwd<DMODE, 4, POSE6D_WGRAD_STAGES>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order);
 }
 
 }  // namespace
@@ -1819,16 +1827,17 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
   Geom gd = pd.g;
   set_bnr(gd, bnr);
   const ReduceJob& carried = rj ? *rj : none;
+  const int order = tune(tn, &pose6d_tuning_t::bwd_order, -1);
   if (phases & 1) {
     switch (pd.mode) {
       case kGemm:
-        rc = launch_bwd_mode<kGemm>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, workspace, carried, s);
+        rc = launch_bwd_mode<kGemm>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, workspace, carried, s, order);
         break;
       case kDgradS2:
-        rc = launch_bwd_mode<kDgradS2>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, workspace, carried, s);
+        rc = launch_bwd_mode<kDgradS2>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, workspace, carried, s, order);
         break;
       default:
-        rc = launch_bwd_mode<kDgrad>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, workspace, carried, s);
+        rc = launch_bwd_mode<kDgrad>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, workspace, carried, s, order);
         break;
     }
   }

@@ -379,6 +379,13 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
     max_bytes = 64ll << 20;   // stem: 16 -> 64 MiB of slabs, 90 -> 65 us
   }
   const int tiles = p6::ceil_div(Cout, p.bm) * p6::ceil_div(Kpad, p.bn);
+  // fp32 128x128 plans with many tiles (layer4's 3x3 convs: 144 tiles over 1568 pixels)
+  // take twice the workgroups: 8 splits of 196 pixels, 207 -> 184 us on 7x7 512->512;
+  // the few-tile KxK shapes keep the default target (profiles/r04_fp32_kxk_splits.txt)
+#ifndef POSE6D_WGRAD_F32_MANY_TILES
+#define POSE6D_WGRAD_F32_MANY_TILES 128   // build-time (A/B): tiles from which the target doubles
+#endif
+  if (p.fast && dtype == POSE6D_DT_F32 && p.bm == 128 && tiles >= POSE6D_WGRAD_F32_MANY_TILES) target *= 2;
   // aim for ~`target` workgroups, each reducing >= min_rows pixels, slabs capped in bytes
   int splits = p6::ceil_div(target, tiles);
   const int max_splits = p6::ceil_div(M, min_rows);
@@ -387,6 +394,8 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
   const int max_by_bytes = (int)(max_bytes / slab);
   if (splits > max_by_bytes) splits = max_by_bytes;
   if (splits < 1) splits = 1;
+  const int forced = tuned(tn, &pose6d_tuning_t::wgrad_splits, 0);   // tools: an explicit split count
+  if (forced >= 1) splits = forced;
   int mps = p6::ceil_div(p6::ceil_div(M, splits), step) * step;
   splits = p6::ceil_div(M, mps);
   p.splits = splits;

@@ -80,7 +80,8 @@ class Tuning(ctypes.Structure):
     """pose6d_tuning_t (include/pose6d.h): explicit plan overrides for the conv
     entry points' *_tuned forms (tests / tuning tools only; -1 = default)."""
     _fields_ = [(n, ctypes.c_int32) for n in ("conv_tile", "conv_stages", "conv_s2", "conv_base", "wgrad_stages",
-                                               "wgrad_base", "bwd_separate", "conv_splitk")]
+                                               "wgrad_base", "bwd_separate", "conv_splitk", "wgrad_splits",
+                                               "bwd_order")]
 
     def __init__(self, **kw):
         super().__init__(*([-1] * len(self._fields_)))

@@ -256,6 +256,8 @@ int pose6d_conv2d_backward(int32_t dtype, const void *x, const void *dy, const v
  *   bwd_separate  1: data and weight gradient as separate launches (not the fused kernel)
  *   conv_splitk   fast path (1x1 / KxK forward, stride-1 data gradient): K-steps of each output tile
  *                 split over this many workgroups of one launch (1 = none)
+ *   wgrad_splits  weight gradient: pixel splits (slabs) of the plan (>= 1; tools only)
+ *   bwd_order     fused backward: 1 = weight-gradient workgroups dispatched first, 0 = data gradient first
  * Split-K plans (the default for long-K convs on small grids, see pose6d_conv_variant
  * >> 16) keep their partial tiles and arrival counters in ONE library-owned device
  * buffer: conv launches on different streams must not run concurrently unless all but
@@ -263,6 +265,7 @@ int pose6d_conv2d_backward(int32_t dtype, const void *x, const void *dy, const v
  * process as the trainer and the DDP path have, is always safe). */
 typedef struct {
   int32_t conv_tile, conv_stages, conv_s2, conv_base, wgrad_stages, wgrad_base, bwd_separate, conv_splitk;
+  int32_t wgrad_splits, bwd_order;
 } pose6d_tuning_t;
 int pose6d_conv2d_fwd_tuned(int32_t dtype, const void *x, const void *w, const float *bias, void *y, float *stats,
                             int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW,

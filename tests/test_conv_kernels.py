@@ -406,6 +406,40 @@ def test_backward_masked_residual(cfg, dtype):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cfg", [(4, 14, 14, 256, 128, 1, 1, 0), (2, 14, 14, 64, 64, 3, 1, 1)])
+def test_backward_dispatch_order_and_splits(cfg, dtype):
+    """The fused backward's dispatch order (pose6d_tuning_t.bwd_order) changes only which
+    workgroups start first: dX and dW bit-identical either way; a forced weight-gradient
+    split count (wgrad_splits, tools only) sums the pixels in another order: dW close to
+    the default plan's."""
+    from pose6d._lib import Tuning, call, query, stream
+    from pose6d.trunk import DTYPES, pack_single
+    N, H, W, Cin, Cout, k, s, p = cfg
+    g = torch.Generator().manual_seed(21)
+    dev, dt = "cuda", DTYPES[dtype]
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    x = _nhwc(torch.randn(N, Cin, H, W, generator=g)).to(dev, dtype)
+    w = (torch.randn(Cout, Cin, k, k, generator=g) * 0.05).to(dev)
+    _, wt = pack_single(w, Cin, dtype)
+    dy = _nhwc(torch.randn(N, Cout, Ho, Wo, generator=g)).to(dev, dtype)
+    outs = []
+    for tn in (Tuning(bwd_order=0), Tuning(bwd_order=1), Tuning(wgrad_splits=1), Tuning(wgrad_splits=3)):
+        ws = torch.empty(query("conv2d_wgrad_workspace_tuned", dt, N, Ho, Wo, Cin, Cout, k, k, tn.ref) // 4 + 1,
+                         device=dev)
+        dx = torch.full_like(x, float("nan"))
+        dw = torch.empty(Cout, Cin, k, k, device=dev)
+        call("conv2d_backward_tuned", dt, x, dy, wt, None, dx, dw, 0, ws, ws.numel() * 4, N, H, W, Cin, Cin, Cout, k,
+             k, s, p, Ho, Wo, tn.ref, stream())
+        torch.cuda.synchronize()
+        outs.append((dx.clone(), dw.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    for dx, dw in outs[2:]:
+        assert torch.equal(dx, outs[0][0])
+        _close(dw.cpu(), outs[0][1].cpu(), 1e-4, f"dW with forced splits {cfg}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_backward_chain_carried_reduce(dtype):
     """pose6d_conv2d_backward_chain over three convs as the trunk issues them: each call
     may leave its weight-gradient slab reduce pending (*deferred) for the next call to
