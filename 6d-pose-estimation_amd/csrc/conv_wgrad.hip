@@ -386,6 +386,13 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
 #define POSE6D_WGRAD_F32_MANY_TILES 128   // build-time (A/B): tiles from which the target doubles
 #endif
   if (p.fast && dtype == POSE6D_DT_F32 && p.bm == 128 && tiles >= POSE6D_WGRAD_F32_MANY_TILES) target *= 2;
+  // fp32 64x64 plans with >= 256 tiles (layer4's 512 -> 2048 / 2048 -> 512 1x1 convs): one
+  // split -- a tile's 1568 pixels in one workgroup, 93 -> 78 us on 7x7 512->2048
+  // (profiles/r04_bwd_plan_sweep.txt)
+#ifndef POSE6D_WGRAD_F32_ONE_SPLIT_TILES
+#define POSE6D_WGRAD_F32_ONE_SPLIT_TILES 256   // build-time (A/B)
+#endif
+  if (p.fast && dtype == POSE6D_DT_F32 && p.bm == 64 && tiles >= POSE6D_WGRAD_F32_ONE_SPLIT_TILES) target = tiles;
   // aim for ~`target` workgroups, each reducing >= min_rows pixels, slabs capped in bytes
   int splits = p6::ceil_div(target, tiles);
   const int max_splits = p6::ceil_div(M, min_rows);
