@@ -1708,9 +1708,10 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
 #endif
   constexpr int WSTEP = sizeof(T) == 4 ? POSE6D_BWD_WSTEP_F32 : 1;
 #ifndef POSE6D_BWD_ORDER
-#define POSE6D_BWD_ORDER 1   // build-time (A/B): 0 = the data gradient always first
+#define POSE6D_BWD_ORDER 1   // build-time (A/B): 0 = the data gradient always first, 2 = the weight gradient
 #endif
-  const int wfirst = order >= 0 ? order : (POSE6D_BWD_ORDER && WSTEP * p6::ceil_div(gw.mps, 64) >= nk);
+  const int wfirst = order >= 0 ? order
+                                : (POSE6D_BWD_ORDER == 2 || (POSE6D_BWD_ORDER && WSTEP * p6::ceil_div(gw.mps, 64) >= nk));
   const int grid = wfirst ? ((nw + 7) & ~7) + nd + rj.nblk : nd_pad + nw + rj.nblk;
   conv_bwd_kernel<DMODE, DS, WS, T><<<grid, kThreads, lds, s>>>(
       (const T*)dy, (const T*)wt, (const T*)dres, (T*)dx, gd, nd, nd_pad, wfirst, (const T*)x, ws, gw, rj);
