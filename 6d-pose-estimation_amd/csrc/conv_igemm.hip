@@ -1829,18 +1829,31 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
   set_bnr(gd, bnr);
   const ReduceJob& carried = rj ? *rj : none;
   const int order = tune(tn, &pose6d_tuning_t::bwd_order, -1);
+  // one weight-gradient split of a 1x1 conv whose K is exactly Cin (layer4's 1x1 convs):
+  // the slab [Cout][Cin] IS the OIHW dW, so the launch writes dW itself and no reduce
+  // follows (the reduce would only have copied it)
+#ifndef POSE6D_WGRAD_DIRECT
+#define POSE6D_WGRAD_DIRECT 1   // build-time (A/B): 0 = every plan through the slab reduce
+#endif
+  const bool direct = POSE6D_WGRAD_DIRECT && gw.splits == 1 && KH == 1 && KW == 1 && gw.Kpad == Cin &&
+                      Cin_real == Cin && !accumulate;
+  float* slab = direct ? dw : workspace;
   if (phases & 1) {
     switch (pd.mode) {
       case kGemm:
-        rc = launch_bwd_mode<kGemm>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, workspace, carried, s, order);
+        rc = launch_bwd_mode<kGemm>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, slab, carried, s, order);
         break;
       case kDgradS2:
-        rc = launch_bwd_mode<kDgradS2>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, workspace, carried, s, order);
+        rc = launch_bwd_mode<kDgradS2>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, slab, carried, s, order);
         break;
       default:
-        rc = launch_bwd_mode<kDgrad>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, workspace, carried, s, order);
+        rc = launch_bwd_mode<kDgrad>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, slab, carried, s, order);
         break;
     }
+  }
+  if (direct) {
+    if (deferred) *deferred = 0;
+    return rc;
   }
   if (deferred) {   // chain mode: this conv's slab reduce rides on the next launch
     *deferred = rc == POSE6D_OK;
