@@ -1386,10 +1386,14 @@ bool fast_ok(int dtype, int mode, const Geom& g) {
 // (tools/conv_bench.py) but lost in the step, so bf16 never picks it.  fp32
 // (MFMA-bound: 4x the MFMAs per byte) takes 128x128 on long K at about one
 // workgroup per CU (profiles/r02_conv_tiles.txt).
+#ifndef POSE6D_TILE4_MIN_K
+#define POSE6D_TILE4_MIN_K 128   // build-time (A/B): the bf16 128x128 tile's minimum K (round 4:
+                                 // 256 -> 128 moved layer2's 128 -> 512 convs onto it, step 4.608 -> 4.601 ms)
+#endif
 int pick_tile_fast(int dtype, int64_t M, int N, int K) {
   const int64_t wg4 = p6::ceil_div(M, 128) * (int64_t)p6::ceil_div(N, 128);
   if (dtype == POSE6D_DT_F32) return (K >= 512 && N >= 128 && wg4 >= 192 && wg4 < 384) ? 4 : 3;
-  return (N >= 128 && K >= 256 && wg4 >= 384) ? 4 : 3;
+  return (N >= 128 && K >= POSE6D_TILE4_MIN_K && wg4 >= 384) ? 4 : 3;
 }
 
 // an override field of a pose6d_tuning_t, or the default (-1 / no struct)
