@@ -74,8 +74,11 @@ struct Geom {
   float* bnr_part2;
   int bnr_rows;
   // split-K (LDS-DMA path, kGemm / kFwd / kDgrad): each output tile's K-steps are
-  // divided over `splits` workgroups (0 or 1 = none); see splitk_merge
+  // divided over `splits` workgroups (0 or 1 = none); see splitk_merge.  sk_cnt /
+  // sk_part: the caller's split-K workspace (arrival counters, partial tiles)
   int splits;
+  int* sk_cnt;
+  float* sk_part;
 };
 
 // ---------------------------------------------------------------------------
@@ -92,25 +95,23 @@ struct Geom {
 // normal epilogue (bias, BN statistics, act, residual).  No workgroup waits for
 // another, so residency does not matter.  This is the hand-off MI355X_MICROARCH.md
 // measures valid with sc1 stores and loads in place of release / acquire fences.
-// The partials and counters are one library-owned device buffer: split-K launches on
-// one device must be stream-ordered (every launch re-arms the counters it used).
-constexpr int64_t kSkWsFloats = (48ll << 20) / 4;   // 48 MiB of partial tiles
-constexpr int kSkMaxTiles = 8192;
-__device__ float g_sk_ws[kSkWsFloats];
-__device__ int g_sk_cnt[kSkMaxTiles];
-
-// the partials of `tiles` tiles x `splits` fit the buffer (host-side plan check)
-inline bool splitk_fits(int64_t tiles, int splits, int tile_elems) {
-  return splits > 1 && tiles <= kSkMaxTiles && tiles * splits * tile_elems <= kSkWsFloats;
-}
+// The partials and counters live in a CALLER-PROVIDED workspace (no library-owned
+// state, so launches on different streams with different workspaces never meet):
+// [kSkCntBytes of arrival counters, one int per output tile][partial tiles].  The
+// counter block has a fixed size so that every plan run on one workspace finds its
+// counters at the same words; the caller zeroes it once (every launch leaves it
+// zero).  Size query: pose6d_conv_splitk_workspace.
+constexpr int kSkMaxTiles = 8192;                       // plans with more tiles never split
+constexpr int64_t kSkCntBytes = (int64_t)kSkMaxTiles * 4;   // 32 KiB
 
 // TM x TN accumulator tiles per wave; PART = floats of one (tile, split) partial
 template <int TM, int TN, int NW>
-__device__ __forceinline__ bool splitk_merge(f32x4 (&acc)[TM][TN], char* smem, int tile, int split, int nsplit) {
+__device__ __forceinline__ bool splitk_merge(f32x4 (&acc)[TM][TN], char* smem, int tile, int split, int nsplit,
+                                             int* cnt, float* part) {
   constexpr int PART = NW * TM * TN * 64 * 4;
   constexpr int SC1 = 16;   // buffer cache-policy bits: sc1
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  float* base = g_sk_ws + (int64_t)tile * nsplit * PART;
+  float* base = part + (int64_t)tile * nsplit * PART;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, nsplit * PART * 4, 0x00020000);
   const int voff = (wave * TM * TN * 64 + lane) * 16;
 #pragma unroll
@@ -122,12 +123,12 @@ __device__ __forceinline__ bool splitk_merge(f32x4 (&acc)[TM][TN], char* smem, i
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave, before the barrier
   __syncthreads();
   int* flag = reinterpret_cast<int*>(smem);
-  if (tid == 0) flag[0] = __hip_atomic_fetch_add(&g_sk_cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) flag[0] = __hip_atomic_fetch_add(&cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   const bool last = flag[0] == nsplit - 1;
   __syncthreads();   // flag read by every wave before the epilogue reuses the LDS
   if (!last) return false;
-  if (tid == 0) __hip_atomic_store(&g_sk_cnt[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) __hip_atomic_store(&cnt[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   f32x4 mine[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -1131,7 +1132,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   }
   asm volatile("s_barrier" ::: "memory");   // every wave done reading the ring before the epilogue reuses it
   if constexpr (SK) {
-    if (nsplit > 1 && !splitk_merge<TM, TN, NW>(acc, smem, tile_id, split, nsplit)) return;
+    if (nsplit > 1 && !splitk_merge<TM, TN, NW>(acc, smem, tile_id, split, nsplit, g.sk_cnt, g.sk_part)) return;
   }
   if constexpr (DUAL)   // acc2 = the block GEMM, acc = the downsample branch
     conv_epilogue<T, BM, BN, 1, NW, true>(acc2, smem, g, bias, nullptr, out, nullptr, m0, n0, -1, acc, pre, false);
@@ -1222,8 +1223,9 @@ int launch_fast(const Geom& g0, const void* src, const void* w, const float* bia
   const int lds = ring > epi ? ring : epi;
   if (MODE == kDgradS2) s2_single_class(g, res, out);
   constexpr bool SK = MODE == kGemm || MODE == kFwd || MODE == kDgrad;
-  if (!SK || !splitk_fits(g.gm * g.gn, g.splits, BM * BN)) g.splits = 1;
-  if (g.splits > nk) g.splits = nk > 0 ? nk : 1;
+  // the plan's split count (choose / splitk_need: <= nk, <= kSkMaxTiles tiles, the
+  // workspace checked by run_conv)
+  if (!SK || g.splits < 1 || !g.sk_cnt) g.splits = 1;
   const int grid = g.gm * g.gn * (MODE == kDgradS2 ? s2_classes(g) : 1) * (g.splits > 1 ? g.splits : 1);
   if constexpr (MODE == kGemm || MODE == kFwd || MODE == kGemmDual) {
     if (g.act) {   // eval BN-act epilogue (pose6d_conv2d_fwd_act)
@@ -1473,21 +1475,47 @@ Plan choose(int dtype, int mode, const Geom& g, bool fused = false, const pose6d
   if (p.stages == 5) p.stages = 4;
   if (cols128 && rows128 && p.stages > 4) p.stages = 4;   // 6 x 32 KiB exceeds the 160 KiB LDS
   if (fused && p.stages == 3) p.stages = 4;   // the fused backward instantiates 2- and 4-slot data gradients
-  // data gradients split only where no fused backward exists for the conv (fp32 KxK: its
-  // weight gradient is register-staged), so fused == separate stays bit-exact elsewhere
-  const bool split_dgrad = dtype == POSE6D_DT_F32 && p.mode == kDgrad;
-  p.g.splits = tune(tn, &pose6d_tuning_t::conv_splitk,
-                    (fwd || split_dgrad) ? default_splits(dtype, p.mode, p.g, fused) : 1);
+  // forwards split by default; data gradients only under an explicit tuning (tests, tools):
+  // the backward entry points take no split-K workspace, and the fused and separate data
+  // gradients stay one plan (one summation order)
+  p.g.splits = tune(tn, &pose6d_tuning_t::conv_splitk, fwd ? default_splits(dtype, p.mode, p.g, fused) : 1);
   if (fused || !(p.mode == kGemm || p.mode == kFwd || p.mode == kDgrad) || p.g.splits < 1) p.g.splits = 1;
+  {
+    const int64_t tiles = (int64_t)p6::ceil_div(p.g.M, rows128 ? 128 : 64) * p6::ceil_div(g.Ncols, cols128 ? 128 : 64);
+    const int nk = fast_nk(p.mode, p.g, dtype == POSE6D_DT_BF16 ? 64 : 32);
+    if (tiles > kSkMaxTiles) p.g.splits = 1;
+    if (p.g.splits > nk) p.g.splits = nk > 0 ? nk : 1;
+  }
   // split-K plans keep their long-K ring depth (the sweep's fastest: 4 slots) unless tuned
   if (p.g.splits > 1 && tune(tn, &pose6d_tuning_t::conv_stages, -1) < 0 && p.stages < 4 && !(cols128 && rows128))
     p.stages = 4;
   return p;
 }
 
+// bytes of split-K workspace a plan needs (0: it does not split K)
+int64_t splitk_need(const Plan& p) {
+  if (!p.fast || p.g.splits <= 1) return 0;
+  const bool rows128 = p.tile <= 1 || p.tile == 4 || p.tile == 5;
+  const bool cols128 = p.tile == 0 || p.tile == 4;
+  const int bm = rows128 ? 128 : 64, bn = cols128 ? 128 : 64;
+  const int64_t tiles = (int64_t)p6::ceil_div(p.g.M, bm) * p6::ceil_div(p.g.Ncols, bn);
+  return kSkCntBytes + tiles * p.g.splits * bm * bn * 4;
+}
+
 int run_conv(int dtype, int mode, const Geom& g, const void* src, const void* w, const float* bias, const void* res,
-             void* out, float* stats, hipStream_t s, const pose6d_tuning_t* tn = nullptr, bool fwd = false) {
-  const Plan p = choose(dtype, mode, g, false, tn, fwd);
+             void* out, float* stats, hipStream_t s, const pose6d_tuning_t* tn = nullptr, bool fwd = false,
+             void* sk_ws = nullptr, int64_t sk_bytes = 0) {
+  Plan p = choose(dtype, mode, g, false, tn, fwd);
+  const int64_t need = splitk_need(p);
+  if (need > 0) {
+    P6_CHECK_ARG(sk_ws != nullptr && sk_bytes >= need,
+                 "conv: this plan splits K over %d workgroups per tile (pose6d_conv_variant >> 16) and needs a split-K "
+                 "workspace of %lld bytes (pose6d_conv_splitk_workspace), got %lld",
+                 p.g.splits, (long long)need, (long long)(sk_ws ? sk_bytes : 0));
+    P6_CHECK_ARG(((uintptr_t)sk_ws & 255) == 0, "conv: the split-K workspace must be 256-byte aligned");
+    p.g.sk_cnt = (int*)sk_ws;
+    p.g.sk_part = (float*)((char*)sk_ws + kSkCntBytes);
+  }
   if (p.fast) return dispatch_fast(dtype, p.mode, p.g, p.tile, p.stages, src, w, bias, res, out, stats, s);
   return dtype == POSE6D_DT_BF16 ? dispatch<bf16>(mode, g, p.tile, src, w, bias, res, out, stats, s)
                                  : dispatch<float>(mode, g, p.tile, src, w, bias, res, out, stats, s);
@@ -1521,15 +1549,17 @@ Geom dgrad_geom(int N, int H, int W, int Cin, int Cout, int KH, int KW, int stri
 
 extern "C" int pose6d_conv2d_fwd(int32_t dtype, const void* x, const void* w, const float* bias, void* y,
                                  float* stats, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH,
-                                 int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, void* stream) {
+                                 int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, void* splitk_ws,
+                                 int64_t splitk_ws_bytes, void* stream) {
   return pose6d_conv2d_fwd_tuned(dtype, x, w, bias, y, stats, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo,
-                                 nullptr, stream);
+                                 nullptr, splitk_ws, splitk_ws_bytes, stream);
 }
 
 extern "C" int pose6d_conv2d_fwd_tuned(int32_t dtype, const void* x, const void* w, const float* bias, void* y,
                                        float* stats, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout,
                                        int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
-                                       const pose6d_tuning_t* tuning, void* stream) {
+                                       const pose6d_tuning_t* tuning, void* splitk_ws, int64_t splitk_ws_bytes,
+                                       void* stream) {
   P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_fwd: bad dtype %d", dtype);
   P6_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cout > 0 && Cout % 8 == 0, "pose6d_conv2d_fwd: bad shape (Cout %% 8)");
   P6_CHECK_ARG(Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1,
@@ -1541,7 +1571,8 @@ extern "C" int pose6d_conv2d_fwd_tuned(int32_t dtype, const void* x, const void*
     P6_CHECK_ARG(g.log2SC >= 0 && Cin % bk == 0, "pose6d_conv2d_fwd: Cin must be 4 or a power of two >= %d (got %d)",
                  bk, Cin);
   if (mode == kGemm) P6_CHECK_ARG(Cin % bk == 0, "pose6d_conv2d_fwd: 1x1 Cin %% %d != 0", bk);
-  return run_conv(dtype, mode, g, x, w, bias, nullptr, y, stats, p6::stream_of(stream), tuning, true);
+  return run_conv(dtype, mode, g, x, w, bias, nullptr, y, stats, p6::stream_of(stream), tuning, true, splitk_ws,
+                  splitk_ws_bytes);
 }
 
 // eval-mode conv + BatchNorm apply (+ residual, + ReLU) in one launch: the store of
@@ -1550,7 +1581,8 @@ extern "C" int pose6d_conv2d_fwd_act(int32_t dtype, const void* x, const void* w
                                      int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW,
                                      int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, const float* scale,
                                      const float* shift, const void* res, const float* res_scale,
-                                     const float* res_shift, int32_t relu, void* stream) {
+                                     const float* res_shift, int32_t relu, void* splitk_ws, int64_t splitk_ws_bytes,
+                                     void* stream) {
   P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_fwd_act: bad dtype %d", dtype);
   P6_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cout > 0 && Cout % 8 == 0, "pose6d_conv2d_fwd_act: bad shape (Cout %% 8)");
   P6_CHECK_ARG(Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1,
@@ -1570,7 +1602,8 @@ extern "C" int pose6d_conv2d_fwd_act(int32_t dtype, const void* x, const void* w
   g.act_shift = shift;
   g.act_rscale = res_scale;
   g.act_rshift = res_shift;
-  return run_conv(dtype, mode, g, x, w, bias, res, out, nullptr, p6::stream_of(stream), nullptr, true);
+  return run_conv(dtype, mode, g, x, w, bias, res, out, nullptr, p6::stream_of(stream), nullptr, true, splitk_ws,
+                  splitk_ws_bytes);
 }
 
 extern "C" int pose6d_conv2d_fwd_act_dual(int32_t dtype, const void* x, const void* w, const void* xd, const void* wd,
@@ -1652,7 +1685,7 @@ int check_bnr(const pose6d_bn_reduce_t* b, const Plan& p, const void* dres, cons
 int dgrad_impl(int32_t dtype, const void* dy, const void* wt, const void* dres, const uint8_t* dres_mask, void* dx,
                int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
                int32_t pad, int32_t Ho, int32_t Wo, void* stream, const pose6d_tuning_t* tn = nullptr,
-               const pose6d_bn_reduce_t* bnr = nullptr) {
+               const pose6d_bn_reduce_t* bnr = nullptr, void* sk_ws = nullptr, int64_t sk_bytes = 0) {
   P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_dgrad: bad dtype %d", dtype);
   P6_CHECK_ARG(stride == 1 || stride == 2, "pose6d_conv2d_dgrad: stride must be 1 or 2");
   P6_CHECK_ARG(Cin % 8 == 0, "pose6d_conv2d_dgrad: Cin %% 8 != 0 (no data gradient for the stem)");
@@ -1667,7 +1700,8 @@ int dgrad_impl(int32_t dtype, const void* dy, const void* wt, const void* dres, 
     if (rc) return rc;
     set_bnr(g, bnr);
   }
-  return run_conv(dtype, mode, g, dy, wt, nullptr, dres, dx, nullptr, p6::stream_of(stream), tn);
+  return run_conv(dtype, mode, g, dy, wt, nullptr, dres, dx, nullptr, p6::stream_of(stream), tn, false, sk_ws,
+                  sk_bytes);
 }
 }  // namespace
 
@@ -1680,9 +1714,10 @@ extern "C" int pose6d_conv2d_dgrad(int32_t dtype, const void* dy, const void* wt
 extern "C" int pose6d_conv2d_dgrad_tuned(int32_t dtype, const void* dy, const void* wt, const void* dres, void* dx,
                                          int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH,
                                          int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
-                                         const pose6d_tuning_t* tuning, void* stream) {
+                                         const pose6d_tuning_t* tuning, void* splitk_ws, int64_t splitk_ws_bytes,
+                                         void* stream) {
   return dgrad_impl(dtype, dy, wt, dres, nullptr, dx, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, stream,
-                    tuning);
+                    tuning, nullptr, splitk_ws, splitk_ws_bytes);
 }
 
 namespace {
@@ -1907,6 +1942,24 @@ extern "C" int pose6d_conv_variant(int32_t dtype, int32_t pass, int32_t N, int32
                            : dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
   const Plan p = choose(dtype, mode, g, false, nullptr, pass == 0);
   return (p.g.splits << 16) | (p.stages << 12) | ((int)p.fast << 8) | (p.mode << 4) | p.tile;
+}
+
+// split-K workspace bytes of a forward (pass 0) / data-gradient (pass 1) conv's plan:
+// 0 when the plan does not split K (then the workspace arguments may be NULL / 0)
+extern "C" int64_t pose6d_conv_splitk_workspace_tuned(int32_t dtype, int32_t pass, int32_t N, int32_t H, int32_t W,
+                                                      int32_t Cin, int32_t Cout, int32_t KH, int32_t KW,
+                                                      int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
+                                                      const pose6d_tuning_t* tuning) {
+  int mode;
+  const Geom g = pass == 0 ? fwd_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode)
+                           : dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
+  return splitk_need(choose(dtype, mode, g, false, tuning, pass == 0));
+}
+
+extern "C" int64_t pose6d_conv_splitk_workspace(int32_t dtype, int32_t pass, int32_t N, int32_t H, int32_t W,
+                                                int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
+                                                int32_t pad, int32_t Ho, int32_t Wo) {
+  return pose6d_conv_splitk_workspace_tuned(dtype, pass, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, nullptr);
 }
 
 // fused backward variant (profiling joins): (1 << 16) | (dgrad mode << 4) | data-gradient

@@ -19,7 +19,7 @@ def plan_buckets(sizes, bucket_elems, tail_elems=0):
     (with the given per-tensor offsets folded in by the caller): a bucket closes
     at the first tensor end that makes it >= bucket_elems; the last bucket ends
     at the buffer end.  tail_elems > 0: a last bucket larger than that is split at
-    the tensor end that leaves the shortest suffix of at most tail_elems (or the last
+    the tensor end that leaves the longest suffix of at most tail_elems (or the last
     tensor alone) -- the last bucket is only ready when the backward ends, so its
     all-reduce is the step's unhidden tail.  Returns [(tensor_index, end_offset)]."""
     ends, start, off = [], 0, 0

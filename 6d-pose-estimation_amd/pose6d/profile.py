@@ -40,14 +40,19 @@ def conv_launches(eng, fused=True):
 
         def fwd(op=op):
             call("conv2d_fwd", dt, op.src.t, op.wp, op.conv.bias, op.out.t, op.stats, B, op.H, op.W, op.cin_pad,
-                 op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, st)
+                 op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, eng.ws_sk, eng.ws_sk_bytes, st)
         out.append((sym, flops, fwd, op.name + ".fwd"))
         bv = query("bwd_variant", dt, B, op.H, op.W, op.cin_pad, op.cout, op.k, op.k, op.stride, op.pad, op.Ho,
                    op.Wo) if (op.needs_dgrad and fused) else 0
         if bv:
             # the step's fused data + weight gradient launch (conv2d_backward phase 1;
             # the slab reduce is its own kernel and row in rocprof)
-            sym = f"conv_bwd_kernel<{(bv >> 4) & 15}, {bv & 15}, 3>"
+            # conv_bwd_kernel<DMODE, DS, WS[, float]>: WS = POSE6D_WGRAD_STAGES (3, bf16) or
+            # POSE6D_WGRAD_STAGES_F32 (2, fp32; csrc/wgrad_body.h)
+            if eng.dtype == torch.float32:
+                sym = f"conv_bwd_kernel<{(bv >> 4) & 15}, {bv & 15}, 2, float>"
+            else:
+                sym = f"conv_bwd_kernel<{(bv >> 4) & 15}, {bv & 15}, 3>"
             dw = torch.empty_like(op.conv.weight)
 
             def bwd(op=op, dw=dw):

@@ -220,7 +220,7 @@ class TrunkEngine:
         e = lambda *s, dt=dtype: torch.empty(*s, device=device, dtype=dt)
         f32 = lambda *s: torch.empty(*s, device=device, dtype=torch.float32)
         self.input.t = e(B, H, W, self.input.C)
-        ws_w, ws_bn = 0, 0
+        ws_w, ws_bn, ws_sk = 0, 0, 0
         for op in self.ops:
             o = op.out
             o.t = e(B, o.H, o.W, o.C)
@@ -238,6 +238,8 @@ class TrunkEngine:
                 op.scale, op.shift, op.mean, op.inv = (f32(op.cout) for _ in range(4))
                 ws_w = max(ws_w, query("conv2d_wgrad_workspace", self.dt, B, op.Ho, op.Wo, op.cin_pad, op.cout, op.k,
                                        op.k))
+                ws_sk = max(ws_sk, query("conv_splitk_workspace", self.dt, 0, B, op.H, op.W, op.cin_pad, op.cout, op.k,
+                                         op.k, op.stride, op.pad, op.Ho, op.Wo))
                 ws_bn = max(ws_bn, (query("bn_bwd_workspace_rows", M) * 2 + 3) * op.cout)
             elif isinstance(op, _ActOp):
                 residual = op.res_act is not None or op.res_conv is not None
@@ -259,6 +261,10 @@ class TrunkEngine:
         self.ws_wgrad2 = f32(max(ws_w // 4, 1))   # ping-pong: a deferred slab reduce reads the other one
         self.ws_bn = f32(max(ws_bn, 1))
         self.ws_fin = None   # pose6d_bn_finalize needs no workspace (one launch)
+        # this engine's split-K workspace (arrival counters zeroed once, re-armed by every
+        # launch; partial tiles): engines on different streams never share one
+        self.ws_sk = torch.zeros(max(ws_sk, 1), device=device, dtype=torch.uint8) if ws_sk else None
+        self.ws_sk_bytes = ws_sk
         self.feat = f32(B, self.feat_dim)
         self.feat_grad_in = None
         self._fold_dev, self._fold_key = None, None
@@ -413,10 +419,11 @@ class TrunkEngine:
                         res = a.res_act.t
                     call("conv2d_fwd_act", dt, op.src.t, op.wp, bias, a.out.t, B, op.H, op.W, op.cin_pad, op.cout,
                          op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, op.scale, op.shift, res, rs, rb, int(a.relu),
-                         st)
+                         self.ws_sk, self.ws_sk_bytes, st)
                     continue
                 call("conv2d_fwd", dt, op.src.t, op.wp, bias, op.out.t, op.stats if training else None, B, op.H,
-                     op.W, op.cin_pad, op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, st)
+                     op.W, op.cin_pad, op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, self.ws_sk,
+                     self.ws_sk_bytes, st)
                 if fold:
                     pass
                 elif op in fin2:

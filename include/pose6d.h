@@ -186,7 +186,23 @@ int pose6d_pack_conv_weights(int32_t dtype, const void *descs, int32_t n_desc, i
 int pose6d_conv_stats_rows(int32_t N, int32_t Ho, int32_t Wo, int32_t Cout);
 int pose6d_conv2d_fwd(int32_t dtype, const void *x, const void *wp, const float *bias, void *y, float *stats,
                       int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW,
-                      int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, void *stream);
+                      int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, void *splitk_ws, int64_t splitk_ws_bytes,
+                      void *stream);
+/* Split-K workspace (caller-provided; the library keeps no device state of its own).
+ * A forward plan on a small grid with a long K loop (pose6d_conv_variant >> 16 > 1)
+ * divides each output tile's K-steps over several workgroups of one launch; their
+ * fp32 partial tiles and the tiles' arrival counters live in splitk_ws:
+ *   bytes = pose6d_conv_splitk_workspace(dtype, pass 0 = forward / 1 = data gradient, geometry...)
+ * (0 = the plan does not split: splitk_ws may be NULL).  Layout: 32 KiB of arrival
+ * counters, then the partial tiles.  The counter block must be ZERO before the first
+ * use of a workspace (e.g. allocate it zeroed); every launch leaves it zero, so one
+ * workspace serves any sequence of stream-ordered convs.  Launches that may run
+ * concurrently (other streams, other threads) need workspaces of their own.  256-byte
+ * aligned.  A plan that splits and gets no (or too small a) workspace fails with
+ * POSE6D_ERR_ARG; data gradients split only under an explicit pose6d_tuning_t. */
+int64_t pose6d_conv_splitk_workspace(int32_t dtype, int32_t pass, int32_t N, int32_t H, int32_t W, int32_t Cin,
+                                     int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho,
+                                     int32_t Wo);
 /* kernel variant a conv launch selects (profiling joins): fwd/dgrad (pass 0/1):
  * (splits << 16) | (stages << 12) | (fast << 8) | (mode << 4) | tile (tile 0..3 = 128x128, 128x64,
  * 64x128, 64x64; mode 0 gemm, 1 im2col, 2 narrow stem, 3 dgrad, 4 stride-2 dgrad
@@ -194,7 +210,9 @@ int pose6d_conv2d_fwd(int32_t dtype, const void *x, const void *wp, const float 
  * of `stages` K-steps, 0 on the register-staged kernel; splits = workgroups per output
  * tile of the in-launch split-K, 1 = none);
  * wgrad (pose6d_wgrad_variant, Cin = the padded channel count): (stages << 12) |
- * (fast << 8) | (BM == 128) << 1 | (BN == 128); fast = LDS-DMA 64x64 kernel. */
+ * (fast << 8) | (BM == 128) << 1 | (BN == 128); fast = the LDS-DMA weight-gradient
+ * kernel (bf16: 64x64 tiles; fp32: 64x64 or 128x128 tiles, bits 1 and 0), 0 = the
+ * register-staged kernel. */
 int pose6d_conv_variant(int32_t dtype, int32_t pass, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout,
                         int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo);
 int pose6d_wgrad_variant(int32_t dtype, int32_t M, int32_t Cout, int32_t K, int32_t Cin);
@@ -204,7 +222,8 @@ int pose6d_wgrad_variant(int32_t dtype, int32_t M, int32_t Cout, int32_t K, int3
 int pose6d_conv2d_fwd_act(int32_t dtype, const void *x, const void *w, const float *bias, void *out, int32_t N,
                           int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
                           int32_t pad, int32_t Ho, int32_t Wo, const float *scale, const float *shift, const void *res,
-                          const float *res_scale, const float *res_shift, int32_t relu, void *stream);
+                          const float *res_scale, const float *res_shift, int32_t relu, void *splitk_ws,
+                          int64_t splitk_ws_bytes, void *stream);
 /* eval-mode output of a torchvision Bottleneck with a downsample branch, ONE launch
  * (replaces, at pose_net_*.py's `self.backbone(x)`, the block's conv3 + bn3 and the
  * downsample conv + bn + add + ReLU):
@@ -258,22 +277,23 @@ int pose6d_conv2d_backward(int32_t dtype, const void *x, const void *dy, const v
  *                 split over this many workgroups of one launch (1 = none)
  *   wgrad_splits  weight gradient: pixel splits (slabs) of the plan (>= 1; tools only)
  *   bwd_order     fused backward: 1 = weight-gradient workgroups dispatched first, 0 = data gradient first
- * Split-K plans (the default for long-K convs on small grids, see pose6d_conv_variant
- * >> 16) keep their partial tiles and arrival counters in ONE library-owned device
- * buffer: conv launches on different streams must not run concurrently unless all but
- * one of them pass conv_splitk = 1 (stream-ordered use, e.g. one compute stream per
- * process as the trainer and the DDP path have, is always safe). */
+ * A tuned plan that splits K needs pose6d_conv_splitk_workspace_tuned(...) bytes of
+ * split-K workspace (see pose6d_conv_splitk_workspace). */
 typedef struct {
   int32_t conv_tile, conv_stages, conv_s2, conv_base, wgrad_stages, wgrad_base, bwd_separate, conv_splitk;
   int32_t wgrad_splits, bwd_order;
 } pose6d_tuning_t;
+int64_t pose6d_conv_splitk_workspace_tuned(int32_t dtype, int32_t pass, int32_t N, int32_t H, int32_t W,
+                                           int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
+                                           int32_t pad, int32_t Ho, int32_t Wo, const pose6d_tuning_t *tuning);
 int pose6d_conv2d_fwd_tuned(int32_t dtype, const void *x, const void *w, const float *bias, void *y, float *stats,
                             int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW,
                             int32_t stride, int32_t pad, int32_t Ho, int32_t Wo, const pose6d_tuning_t *tuning,
-                            void *stream);
+                            void *splitk_ws, int64_t splitk_ws_bytes, void *stream);
 int pose6d_conv2d_dgrad_tuned(int32_t dtype, const void *dy, const void *wt, const void *dres, void *dx, int32_t N,
                               int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
-                              int32_t pad, int32_t Ho, int32_t Wo, const pose6d_tuning_t *tuning, void *stream);
+                              int32_t pad, int32_t Ho, int32_t Wo, const pose6d_tuning_t *tuning, void *splitk_ws,
+                              int64_t splitk_ws_bytes, void *stream);
 int64_t pose6d_conv2d_wgrad_workspace_tuned(int32_t dtype, int32_t N, int32_t Ho, int32_t Wo, int32_t Cin,
                                             int32_t Cout, int32_t KH, int32_t KW, const pose6d_tuning_t *tuning);
 int pose6d_conv2d_wgrad_tuned(int32_t dtype, const void *x, const void *dy, float *dw, int32_t accumulate,
@@ -287,7 +307,10 @@ int pose6d_conv2d_backward_tuned(int32_t dtype, const void *x, const void *dy, c
                                  const pose6d_tuning_t *tuning, void *stream);
 /* pose6d_conv2d_backward in phases (profiling): bit 0 = the gradient launch(es) that
  * fill the fp32 slabs (and dx), bit 1 = the slab reduce into dw; 3 = the whole call.
- * On the unfused path bit 0 runs the complete dgrad + wgrad and bit 1 nothing. */
+ * On the unfused path bit 0 runs the complete dgrad + wgrad and bit 1 nothing.  A
+ * fused 1x1 conv whose weight gradient has ONE split and K = Cin = Cin_real, not
+ * accumulating (layer4's 1x1 convs), writes dw directly during bit 0 (its single slab
+ * is the OIHW gradient): bit 1 then does nothing. */
 int pose6d_conv2d_backward_ex(int32_t dtype, const void *x, const void *dy, const void *wt, const void *dres,
                               void *dx, float *dw, int32_t accumulate, float *workspace, int64_t ws_bytes, int32_t N,
                               int32_t H, int32_t W, int32_t Cin, int32_t Cin_real, int32_t Cout, int32_t KH,
@@ -301,7 +324,8 @@ int pose6d_conv2d_backward_ex(int32_t dtype, const void *x, const void *dy, cons
  * `prev` (NULL = none; its slabs must be in a different workspace) and (b) when
  * this conv runs the fused kernel, leaves its OWN reduce pending: *deferred = 1,
  * and the caller passes it as `prev` to the next call or flushes it with
- * pose6d_wgrad_reduce.  *deferred = 0: this conv's dW is complete. */
+ * pose6d_wgrad_reduce.  *deferred = 0: this conv's dW is complete (also the case of
+ * the direct-dW plans described at pose6d_conv2d_backward_ex). */
 typedef struct {
   const float *ws;
   float *dw;

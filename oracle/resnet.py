@@ -58,6 +58,15 @@ def trunk(x, P, pre, training):
     return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
 
 
+def _trunk_or(features, x, P, pre, training):
+    """The trunk's (B, 2048) features, or -- when `features` maps this trunk's
+    prefix to a tensor -- that tensor (the trunk hook the model fixture of
+    tests/golden/models.npz is checked through: it pins everything around the trunk)."""
+    if features is not None and pre in features:
+        return features[pre]
+    return trunk(x, P, pre, training)
+
+
 def _lin(x, P, name):
     return F.linear(x, P[name + ".weight"], P[name + ".bias"])
 
@@ -103,17 +112,18 @@ def pinhole_rgb_geometric(z, bbox_center, K):
     return torch.cat([(u - cx) * z / fx, (v - cy) * z / fy, z], dim=1)
 
 
-def forward_rgb(P, x, training):
+def forward_rgb(P, x, training, features=None):
     """pose_net_rgb.py:56-65."""
-    f = trunk(x, P, "backbone", training)
+    f = _trunk_or(features, x, P, "backbone", training)
     rot = normalize(bn_mlp(f, P, "rot_head", [2048, 2048, 1024, 512, 4], training))
     trans = bn_mlp(f, P, "trans_head", [2048, 2048, 1024, 512, 3], training)
     return rot, trans
 
 
-def forward_rgbd_geometric(P, rgb, depth=None, depth_raw=None, bbox_center=None, K=None, training=False):
+def forward_rgbd_geometric(P, rgb, depth=None, depth_raw=None, bbox_center=None, K=None, training=False,
+                           features=None):
     """pose_net_rgbd_geometric.py:40-54."""
-    f = trunk(rgb, P, "backbone", training)
+    f = _trunk_or(features, rgb, P, "backbone", training)
     rot = normalize(bn_mlp(f, P, "rot_head", [2048, 1024, 512, 4], training))
     if depth_raw is not None and bbox_center is not None and K is not None:
         trans = pinhole_rgbd_geometric(depth_raw, bbox_center, K)
@@ -132,9 +142,9 @@ def z_backbone(x, P, training):
     return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
 
 
-def forward_rgb_geometric(P, rgb, bbox_center=None, K=None, training=False):
+def forward_rgb_geometric(P, rgb, bbox_center=None, K=None, training=False, features=None):
     """pose_net_rgb_geometric.py:70-91."""
-    f = trunk(rgb, P, "rgb_backbone", training)
+    f = _trunk_or(features, rgb, P, "rgb_backbone", training)
     r = bn_mlp(f, P, "rot_head", [2048, 1024, 512, 4], training)
     rot = r / (torch.norm(r, dim=1, keepdim=True) + 1e-8)
     z = z_backbone(rgb, P, training)
@@ -169,11 +179,11 @@ def _gelu_head(x, P, pre):
     return _lin(x, P, pre + ".6")
 
 
-def forward_rgbd(P, rgb, depth, depth_raw=None, bbox_center=None, K=None, training=False):
+def forward_rgbd(P, rgb, depth, depth_raw=None, bbox_center=None, K=None, training=False, features=None):
     """pose_net_rgbd.py:118-142."""
     B = rgb.size(0)
-    r = _ln(trunk(rgb, P, "rgb_backbone", training), P, "rgb_norm")
-    d = _ln(trunk(depth, P, "depth_backbone", training), P, "depth_norm")
+    r = _ln(_trunk_or(features, rgb, P, "rgb_backbone", training), P, "rgb_norm")
+    d = _ln(_trunk_or(features, depth, P, "depth_backbone", training), P, "depth_norm")
     r_enh = r + cross_attention(r, d, P)
     x = torch.cat([r_enh, d], dim=1)
     x = F.gelu(_ln(_lin(x, P, "fusion.0"), P, "fusion.1"))

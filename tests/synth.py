@@ -143,3 +143,68 @@ def xattn_weights(D, seed):
         sd[n + ".weight"] = torch.randn(D, D, generator=g) * D ** -0.5
         sd[n + ".bias"] = torch.randn(D, generator=g) * 0.1
     return sd
+
+
+TRUNK_PREFIXES = ("backbone.", "rgb_backbone.", "depth_backbone.")
+
+
+def head_weights(shapes, seed):
+    """Parameters and BN/LN buffers of a PoseNet's reference-owned layers (every
+    state_dict key outside the ResNet50 trunks) from a seeded CPU generator, in
+    sorted key order: >= 2-D weights N(0, 1/fan_in), 1-D weights 1 + N(0, 0.1^2),
+    biases N(0, 0.1^2), running_mean N(0, 0.1^2), running_var U[0.5, 1.5);
+    num_batches_tracked is left alone.  `shapes`: {key: shape}.  The model fixture
+    (tools/gen_goldens.py gen_models) was made with it; the fixture stores the
+    checksums the tests compare against."""
+    import torch
+    g = torch.Generator().manual_seed(seed)
+    sd = {}
+    for k in sorted(shapes):
+        if k.startswith(TRUNK_PREFIXES) or k.endswith("num_batches_tracked"):
+            continue
+        shp = tuple(shapes[k])
+        if k.endswith("running_mean"):
+            v = torch.randn(shp, generator=g) * 0.1
+        elif k.endswith("running_var"):
+            v = torch.rand(shp, generator=g) + 0.5
+        elif len(shp) >= 2:
+            fan_in = 1
+            for s in shp[1:]:
+                fan_in *= s
+            v = torch.randn(shp, generator=g) * fan_in ** -0.5
+        elif k.endswith(".weight"):
+            v = 1.0 + torch.randn(shp, generator=g) * 0.1
+        else:
+            v = torch.randn(shp, generator=g) * 0.1
+        sd[k] = v
+    return sd
+
+
+def model_inputs(B, seed):
+    """Seeded CPU inputs of the model fixture: rgb N(0,1) (B,3,224,224), depth U[0,1)
+    (B,1,224,224), depth_raw U[0.3,1.6) m with ~5 % zeros (B,224,224), bbox centre
+    U[0,223)^2, K with fx, fy U[400,800), cx, cy U[80,144), unit gt quaternion,
+    gt translation around (0, 0, 0.8) m."""
+    import torch
+    g = torch.Generator().manual_seed(seed)
+    rgb = torch.randn(B, 3, 224, 224, generator=g)
+    depth = torch.rand(B, 1, 224, 224, generator=g)
+    depth_raw = torch.rand(B, 224, 224, generator=g) * 1.3 + 0.3
+    depth_raw[torch.rand(B, 224, 224, generator=g) < 0.05] = 0.0
+    bbox = torch.rand(B, 2, generator=g) * 223
+    K = torch.zeros(B, 3, 3)
+    K[:, 0, 0] = torch.rand(B, generator=g) * 400 + 400
+    K[:, 1, 1] = torch.rand(B, generator=g) * 400 + 400
+    K[:, 0, 2] = torch.rand(B, generator=g) * 64 + 80
+    K[:, 1, 2] = torch.rand(B, generator=g) * 64 + 80
+    K[:, 2, 2] = 1.0
+    gt_rot = torch.nn.functional.normalize(torch.randn(B, 4, generator=g), dim=1)
+    gt_trans = torch.randn(B, 3, generator=g) * 0.1 + torch.tensor([0.0, 0.0, 0.8])
+    return {"rgb": rgb, "depth": depth, "depth_raw": depth_raw, "bbox": bbox, "K": K,
+            "gt_rot": gt_rot, "gt_trans": gt_trans}
+
+
+def tensor_checksum(t):
+    """(sum, sum of squares) in fp64: detects a drifted generator stream."""
+    a = t.detach().cpu().numpy().astype(np.float64).ravel()   # numpy: independent of torch's thread count
+    return [float(a.sum()), float((a * a).sum())]

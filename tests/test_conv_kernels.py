@@ -29,6 +29,17 @@ def _close(got, ref, rtol, what):
     assert not bool(bad.any()), f"{what}: max err {err.max().item():.3e} (scale {scale:.3e}), {int(bad.sum())} bad"
 
 
+_SKWS = {}
+
+
+def skws(i=0):
+    """A zeroed split-K workspace (pose6d_conv_splitk_workspace; 64 MiB covers every
+    plan these tests force): (tensor, bytes) for the conv entry points."""
+    if i not in _SKWS:
+        _SKWS[i] = torch.zeros(64 << 20, device="cuda", dtype=torch.uint8)
+    return _SKWS[i], _SKWS[i].numel()
+
+
 def _nhwc(t, cpad=None):
     t = t.permute(0, 2, 3, 1).contiguous()
     if cpad is not None and cpad > t.shape[-1]:
@@ -61,7 +72,7 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
     rows = query("conv_stats_rows", N, Ho, Wo, Cout)
     stats = torch.empty(2, Cout, rows, device=dev)
     call("conv2d_fwd", dt, xd, wp, b.to(dev) if b is not None else None, y, stats, N, H, W, cpad, Cout, k, k, s, p,
-         Ho, Wo, stream())
+         Ho, Wo, *skws(), stream())
     xr = x.clone().requires_grad_(True)
     wr = w.clone().requires_grad_(True)
     yr = F.conv2d(xr, wr, b, stride=s, padding=p)
@@ -142,8 +153,10 @@ def test_conv_fast_variants_bit_identical(cfg):
         y = torch.empty(N, Ho, Wo, Cout, device=dev, dtype=dtype)
         dx = torch.empty(N, H, W, Cin, device=dev, dtype=dtype)
         dw = torch.empty(Cout, Cin, k, k, device=dev)
-        call("conv2d_fwd_tuned", dt, x, wp, None, y, None, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, tn.ref, stream())
-        call("conv2d_dgrad_tuned", dt, dy, wt, dres, dx, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, tn.ref, stream())
+        call("conv2d_fwd_tuned", dt, x, wp, None, y, None, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, tn.ref, *skws(),
+             stream())
+        call("conv2d_dgrad_tuned", dt, dy, wt, dres, dx, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, tn.ref, *skws(),
+             stream())
         call("conv2d_wgrad_tuned", dt, x, dy, dw, 0, ws, ws.numel() * 4, N, H, W, Cin, Cin, Cout, k, k, s, p, Ho, Wo,
              tn.ref, stream())
         torch.cuda.synchronize()
@@ -152,7 +165,7 @@ def test_conv_fast_variants_bit_identical(cfg):
     y0, dx0, dw0 = run()
     # the plain (untuned) entry points are the default plan
     y = torch.empty(N, Ho, Wo, Cout, device=dev, dtype=dtype)
-    call("conv2d_fwd", dt, x, wp, None, y, None, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream())
+    call("conv2d_fwd", dt, x, wp, None, y, None, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, *skws(), stream())
     torch.cuda.synchronize()
     assert torch.equal(y.cpu(), y0)
     variants = [dict(conv_stages=st, conv_tile=t) for st in (2, 3, 4, 6) for t in (0, 1, 3, 4, 5)]
@@ -236,9 +249,12 @@ def test_conv_splitk(cfg, dtype):
         y = torch.empty(N, Ho, Wo, Cout, device=dev, dtype=dtype)
         st = torch.empty(2, Cout, rows, device=dev)
         dx = torch.empty(N, H, W, Cin, device=dev, dtype=dtype)
-        call("conv2d_fwd_tuned", dt, xd, wp, None, y, st, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, tn.ref, stream())
-        call("conv2d_dgrad_tuned", dt, dyd, wt, dresd, dx, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, tn.ref,
+        need = query("conv_splitk_workspace_tuned", dt, 0, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, tn.ref)
+        assert need == 0 or need <= skws()[1]
+        call("conv2d_fwd_tuned", dt, xd, wp, None, y, st, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, tn.ref, *skws(),
              stream())
+        call("conv2d_dgrad_tuned", dt, dyd, wt, dresd, dx, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, tn.ref,
+             *skws(), stream())
         torch.cuda.synchronize()
         return y.cpu(), st.cpu(), dx.cpu()
 
@@ -262,6 +278,67 @@ def test_conv_splitk(cfg, dtype):
         again = run(conv_splitk=splits)
         for a, b, what in zip(ref, again, ("fwd", "stats", "dgrad")):
             assert torch.equal(a, b), f"{what}: repeated launch differs (splits={splits})"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv_splitk_workspace_contract(dtype):
+    """The split-K scratch is the caller's (include/pose6d.h, pose6d_conv_splitk_workspace):
+    a plan that splits refuses a missing / short workspace, and split-K forwards running
+    CONCURRENTLY on two streams, each with its own workspace, give the serial bits."""
+    from pose6d._lib import Pose6dError, call, query
+    from pose6d.trunk import DTYPES, pack_single
+    dt = DTYPES[dtype]
+    shapes = [(32, 7, 7, 512, 512, 3, 1, 1), (32, 7, 7, 2048, 512, 1, 1, 0)]   # layer4: default plans split
+    g = torch.Generator().manual_seed(5)
+    cases = []
+    for N, H, W, Cin, Cout, k, s, p in shapes:
+        Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        assert query("conv_variant", dt, 0, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo) >> 16 > 1
+        need = query("conv_splitk_workspace", dt, 0, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo)
+        assert need > 32768
+        x = torch.randn(N, H, W, Cin, generator=g).to("cuda", dtype)
+        w = (torch.randn(Cout, Cin, k, k, generator=g) * (1.0 / (Cin * k * k)) ** 0.5).cuda()
+        wp, _ = pack_single(w, Cin, dtype, with_t=False)
+        cases.append(((N, H, W, Cin, Cout, k, k, s, p, Ho, Wo), x, wp, need))
+    args, x, wp, need = cases[0]
+    y = torch.empty(args[0], args[9], args[10], args[4], device="cuda", dtype=dtype)
+    st = ctypes_stream(torch.cuda.current_stream())
+    with pytest.raises(Pose6dError, match="split-K workspace"):
+        call("conv2d_fwd", dt, x, wp, None, y, None, *args, None, 0, st)
+    small = torch.zeros(need - 256, device="cuda", dtype=torch.uint8)
+    with pytest.raises(Pose6dError, match="split-K workspace"):
+        call("conv2d_fwd", dt, x, wp, None, y, None, *args, small, small.numel(), st)
+
+    def run_all(streams, wss, reps):
+        torch.cuda.synchronize()
+        outs = [[torch.empty(a[0], a[9], a[10], a[4], device="cuda", dtype=dtype) for _ in range(reps)]
+                for a, _, _, _ in cases]
+        for r in range(reps):
+            for i, (a, xx, ww, _) in enumerate(cases):
+                sidx = (i + r) % len(streams)
+                with torch.cuda.stream(streams[sidx]):
+                    call("conv2d_fwd", dt, xx, ww, None, outs[i][r], None, *a, wss[sidx], wss[sidx].numel(),
+                         ctypes_stream(streams[sidx]))
+        torch.cuda.synchronize()
+        return [[o.cpu() for o in row] for row in outs]
+
+    big = max(c[3] for c in cases)
+    ws_a = torch.zeros(big, device="cuda", dtype=torch.uint8)
+    ws_b = torch.zeros(big, device="cuda", dtype=torch.uint8)
+    serial = run_all([torch.cuda.current_stream()], [ws_a], 1)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    conc = run_all([s1, s2], [ws_a, ws_b], 6)
+    for i in range(len(cases)):
+        for r in range(6):
+            assert torch.equal(conc[i][r], serial[i][0]), f"shape {i} rep {r}: concurrent split-K differs"
+    # the counters are left zero (re-armed by every launch)
+    assert int(ws_a[:32768].count_nonzero()) == 0 and int(ws_b[:32768].count_nonzero()) == 0
+
+
+def ctypes_stream(s):
+    import ctypes
+    return ctypes.c_void_p(s.cuda_stream)
 
 
 @pytest.mark.gpu

@@ -42,8 +42,9 @@ def test_invalid_args_reported_without_gpu():
 def test_conv_plan_query_reports_split_k():
     """pose6d_conv_variant (host-only plan query): (splits << 16) | (stages << 12) |
     (fast << 8) | (mode << 4) | tile.  Split-K is taken by default only for long-K convs
-    on grids of <= 256 64x64 tiles (layer4 at batch 32), and the data gradient of a bf16
-    conv never splits (fused and separate backward stay bit-identical)."""
+    on grids of <= 256 64x64 tiles (layer4 at batch 32); data gradients never split by
+    default (fused and separate backward stay one plan, and the backward entry points take
+    no split-K workspace); pose6d_conv_splitk_workspace sizes the caller's scratch."""
     from pose6d._lib import DT_BF16, DT_F32, query
 
     def splits(dt, pas, N, H, Cin, Cout, k, s):
@@ -56,8 +57,17 @@ def test_conv_plan_query_reports_split_k():
         assert splits(dt, 0, 32, 7, 2048, 512, 1, 1) == 2     # layer4 2048 -> 512 1x1
         assert splits(dt, 0, 32, 56, 64, 256, 1, 1) == 1      # layer1: big grid
         assert splits(dt, 0, 32, 14, 256, 1024, 1, 1) == 1    # short K
-    assert splits(DT_BF16, 1, 32, 7, 512, 512, 3, 1) == 1    # bf16 data gradient: never split
-    assert splits(DT_F32, 1, 32, 7, 512, 512, 3, 1) == 2     # fp32 KxK data gradient (no fused backward)
+    for dt in (DT_BF16, DT_F32):                             # data gradients: split only when tuned
+        assert splits(dt, 1, 32, 7, 512, 512, 3, 1) == 1
+
+    # the split-K workspace a plan needs (caller-provided: 32 KiB of counters + partial tiles)
+    def ws(dt, pas, N, H, Cin, Cout, k, s):
+        p = k // 2
+        Ho = (H + 2 * p - k) // s + 1
+        return query("conv_splitk_workspace", dt, pas, N, H, H, Cin, Cout, k, k, s, p, Ho, Ho)
+    assert ws(DT_BF16, 0, 32, 7, 512, 512, 3, 1) == 32768 + 200 * 2 * 64 * 64 * 4
+    assert ws(DT_BF16, 0, 32, 56, 64, 256, 1, 1) == 0
+    assert ws(DT_F32, 1, 32, 7, 512, 512, 3, 1) == 0
 
 
 def test_dual_eval_launch_rejects_split_k_geometry():

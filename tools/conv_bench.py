@@ -106,26 +106,27 @@ def main():
                                    Tuning(wgrad_base=1).ref), 256 << 20) // 4,
                          device=dev)
         dw = torch.empty(Cout, Cin, k, k, device=dev)
+        skw = torch.zeros(64 << 20, device=dev, dtype=torch.uint8)   # split-K workspace (caller-provided)
         flops = 2.0 * B * Ho * Wo * Cout * Cin * k * k
         sc, sh = torch.rand(Cout, device=dev) + 0.5, torch.randn(Cout, device=dev) * 0.1
         res = torch.randn(B, Ho, Wo, Cout, device=dev).to(dtype) if "fwdactres" in a.passes else None
         fns = {
             "fwd": lambda: call("conv2d_fwd_tuned", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k, k, s, p, Ho,
-                                Wo, TUNE.ref, stream()),
+                                Wo, TUNE.ref, skw, skw.numel(), stream()),
             # no BN statistics (as in eval without the fold)
             "fwdns": lambda: call("conv2d_fwd", dt, x, wp, None, y, None, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo,
-                                  stream()),
+                                  skw, skw.numel(), stream()),
             # each call behind a 512 MB write (caches hold none of the conv's operands), minus that write's time
             "fwdcold": lambda: (flush.zero_(), call("conv2d_fwd", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k,
-                                                    k, s, p, Ho, Wo, stream())),
+                                                    k, s, p, Ho, Wo, skw, skw.numel(), stream())),
             "flush": lambda: flush.zero_(),
             # eval epilogue: BN (+ residual) + ReLU applied before the store (pose6d_conv2d_fwd_act)
             "fwdact": lambda: call("conv2d_fwd_act", dt, x, wp, None, y, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, sc,
-                                   sh, None, None, None, 1, stream()),
+                                   sh, None, None, None, 1, skw, skw.numel(), stream()),
             "fwdactres": lambda: call("conv2d_fwd_act", dt, x, wp, None, y, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo,
-                                      sc, sh, res, None, None, 1, stream()),
+                                      sc, sh, res, None, None, 1, skw, skw.numel(), stream()),
             "dgrad": lambda: call("conv2d_dgrad_tuned", dt, dy, wt, None, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo,
-                                  TUNE.ref, stream()),
+                                  TUNE.ref, skw, skw.numel(), stream()),
             "dgradip": lambda: call("conv2d_dgrad", dt, dy, wt, dx, dx, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, stream()),
             "bwdip": lambda: call("conv2d_backward", dt, x, dy, wt, dx, dx, dw, 0, ws, ws.numel() * 4, B, H, W, Cin,
                                   Cin, Cout, k, k, s, p, Ho, Wo, stream()),

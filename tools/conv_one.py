@@ -28,10 +28,11 @@ def main():
     stats = torch.empty(query("conv_stats_rows", B, Ho, Wo, Cout), 2, Cout, device=dev)
     ws = torch.empty(query("conv2d_wgrad_workspace", dt, B, Ho, Wo, Cin, Cout, k, k) // 4 + 1, device=dev)
     dw = torch.empty(Cout, Cin, k, k, device=dev)
+    skw = torch.zeros(64 << 20, device=dev, dtype=torch.uint8)   # split-K workspace (caller-provided)
     st = stream()
     for _ in range(reps):
         if ps == "fwd":
-            call("conv2d_fwd", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, st)
+            call("conv2d_fwd", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo, skw, skw.numel(), st)
         elif ps == "wgrad":
             call("conv2d_wgrad", dt, x, dy, dw, 0, ws, ws.numel() * 4, B, H, W, Cin, Cin, Cout, k, k, s, p, Ho, Wo,
                  st)

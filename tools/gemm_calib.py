@@ -63,8 +63,9 @@ def main():
         stats = torch.empty(query("conv_stats_rows", B, H, H, Cout), 2, Cout, device=dev)
         ws = torch.empty(query("conv2d_wgrad_workspace", dt, B, H, H, Cin, Cout, 1, 1) // 4 + 1, device=dev)
         dwf = torch.empty(Cout, Cin, 1, 1, device=dev)
+        skw = torch.zeros(64 << 20, device=dev, dtype=torch.uint8)   # split-K workspace (caller-provided)
         t_f = gtime(lambda: call("conv2d_fwd", dt, x, wp, None, yo, stats, B, H, H, Cin, Cout, 1, 1, 1, 0, H, H,
-                                 stream()))
+                                 skw, skw.numel(), stream()))
         t_d = gtime(lambda: call("conv2d_dgrad", dt, dy, wtp, None, dxo, B, H, H, Cin, Cout, 1, 1, 1, 0, H, H,
                                  stream()))
         t_w = gtime(lambda: call("conv2d_wgrad", dt, x, dy, dwf, 0, ws, ws.numel() * 4, B, H, H, Cin, Cin, Cout, 1,

@@ -14,9 +14,18 @@ absent from this image.  Their torchvision-free parts -- `CrossModalAttention`
 (pose_net_rgbd_geometric.py:56-85, pose_net_rgb_geometric.py:93-109) -- are run
 by importing those files against a `torchvision` placeholder whose every
 attribute access RAISES: the module-level import succeeds, and no third-party
-arithmetic can enter a fixture (nothing here constructs a model, so nothing asks
-for `models.resnet50`).  The ResNet50 trunk stays parity-unpinned (DESIGN.md
-"Oracle").
+arithmetic can enter a fixture (nothing there constructs a model, so nothing asks
+for `models.resnet50`).
+
+The four model classes themselves (gen_models -> tests/golden/models.npz) run with
+a `torchvision.models` stand-in whose resnet50() is a small plain-torch network with
+ResNet's child layout (_StandInResNet): the fixture records the features that
+stand-in hands the reference's own code and everything downstream of them, so the
+heads, fusion, z-CNN, normalisations and pinholes are pinned while no value depends
+on a restatement of torchvision.  The ResNet50 trunk itself stays parity-unpinned
+(DESIGN.md "Oracle").
+
+    python tools/gen_goldens.py models     # only tests/golden/models.npz
 """
 import importlib.util
 import json
@@ -295,14 +304,202 @@ def gen_model_parts():
     np.savez_compressed(os.path.join(OUT, "model_parts.npz"), **out)
 
 
+class _StandInResNet(torch.nn.Module):
+    """Trunk stand-in for the model fixture: ResNet's child layout (conv1, bn1, relu,
+    maxpool, layer1-4, avgpool, fc -- so `children()[:-1]` and the depth model's
+    `.conv1` swap, pose_net_rgbd.py:52-61, work unchanged) built from plain torch
+    layers, (B, C, 224, 224) -> (B, 2048, 1, 1).  It is NOT torchvision's ResNet50
+    and none of its arithmetic is pinned: the fixture records the features it hands
+    the reference's own code, and the tests feed those recorded features -- not a
+    trunk -- to the oracle and to the drop-in modules."""
+
+    def __init__(self):
+        super().__init__()
+        nn = torch.nn
+        self.conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, 2, 1)
+        self.layer1 = nn.Sequential(nn.Conv2d(64, 256, 1, bias=False), nn.ReLU())
+        self.layer2 = nn.Sequential(nn.Conv2d(256, 512, 1, stride=2, bias=False), nn.ReLU())
+        self.layer3 = nn.Sequential(nn.Conv2d(512, 1024, 1, stride=2, bias=False), nn.ReLU())
+        self.layer4 = nn.Sequential(nn.Conv2d(1024, 2048, 1, stride=2, bias=False), nn.ReLU())
+        self.avgpool = nn.AdaptiveAvgPool2d(1)
+        self.fc = nn.Linear(2048, 1000)
+
+
+class _StandInModels(types.ModuleType):
+    """`torchvision.models` for the fixture run: resnet50(weights=None) -> _StandInResNet;
+    ResNet50_Weights.DEFAULT exists only so the `pretrained` expression evaluates
+    (the fixture constructs every model with pretrained=False)."""
+
+    def __init__(self, name):
+        super().__init__(name)
+        self.ResNet50_Weights = types.SimpleNamespace(DEFAULT="IMAGENET1K_V2 (never loaded)")
+
+    @staticmethod
+    def resnet50(weights=None):
+        if weights is not None:
+            raise RuntimeError("the fixture never loads pretrained weights")
+        return _StandInResNet()
+
+
+def _load_models_standin():
+    tv = types.ModuleType("torchvision")
+    tvm = _StandInModels("torchvision.models")
+    tv.models = tvm
+    saved = {k: sys.modules.get(k) for k in ("torchvision", "torchvision.models")}
+    sys.modules["torchvision"], sys.modules["torchvision.models"] = tv, tvm
+    try:
+        mods = {"PoseNetRGB": _load("ref_sm_rgb", "models/pose_net_rgb.py").PoseNetRGB,
+                "PoseNetRGBGeometric": _load("ref_sm_rgb_geo", "models/pose_net_rgb_geometric.py").PoseNetRGBGeometric,
+                "PoseNetRGBD": _load("ref_sm_rgbd", "models/pose_net_rgbd.py").PoseNetRGBD,
+                "PoseNetRGBDGeometric": _load("ref_sm_rgbd_geo",
+                                              "models/pose_net_rgbd_geometric.py").PoseNetRGBDGeometric}
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    return mods
+
+
+# model -> (trunk attributes, forward argument names)
+MODEL_SPECS = {
+    "PoseNetRGB": (("backbone",), ("rgb",)),
+    "PoseNetRGBGeometric": (("rgb_backbone",), ("rgb", "bbox", "K")),
+    "PoseNetRGBD": (("rgb_backbone", "depth_backbone"), ("rgb", "depth")),
+    "PoseNetRGBDGeometric": (("backbone",), ("rgb", "depth", "depth_raw", "bbox", "K")),
+}
+MODEL_B = 8
+MODEL_INPUT_SEED = 4242
+MODEL_WEIGHT_SEED = {"PoseNetRGB": 101, "PoseNetRGBGeometric": 102, "PoseNetRGBD": 103, "PoseNetRGBDGeometric": 104}
+GRAD_ROWS = 4
+
+
+def _record_grads(out, key, named):
+    for k, p in named:
+        if p.grad is None:
+            continue
+        g = p.grad.detach().numpy()
+        out[f"{key}/grad/{k}"] = g[:GRAD_ROWS] if g.ndim >= 2 else g
+        out[f"{key}/gradnorm/{k}"] = np.asarray(np.linalg.norm(g.astype(np.float64)), np.float64)
+        out[f"{key}/gradsum/{k}"] = np.asarray(g.astype(np.float64).sum(), np.float64)
+
+
+def gen_models(ref_pl):
+    """The reference's four PoseNet classes run end to end with the trunk stand-in:
+    every reference-owned layer around the trunk (heads, BN1d / LayerNorm MLPs, the
+    normalisations incl. q/(||q||+1e-8), the z-CNN + z-MLP, CrossModalAttention +
+    LN/GELU fusion, the pinholes) in eval mode and in train mode (Dropout modules
+    in eval, BN with batch statistics), plus PoseLoss(1, 10) and its backward.
+    Recorded: the trunk features, outputs, loss, feature gradients, parameter
+    gradients (first rows, norm, sum), BN running statistics after the step, the
+    z-CNN features; and the reference's own init constants (translation / z biases,
+    xavier statistics of PoseNetRGBD's MLPs)."""
+    from tests.synth import head_weights, model_inputs, tensor_checksum
+    classes = _load_models_standin()
+    inp = model_inputs(MODEL_B, MODEL_INPUT_SEED)
+    out = {}
+    for k, v in inp.items():
+        out[f"inputs/checksum/{k}"] = np.asarray(tensor_checksum(v), np.float64)
+    for k in ("bbox", "K", "gt_rot", "gt_trans"):
+        out[f"inputs/{k}"] = inp[k].numpy()
+    for name, (trunks, argnames) in MODEL_SPECS.items():
+        # --- init constants of the reference's own constructor --------------------------
+        torch.manual_seed(0)
+        fresh = classes[name](pretrained=False)
+        if hasattr(fresh, "trans_head"):
+            out[f"{name}/init/trans_bias"] = fresh.trans_head[-1].bias.detach().numpy().copy()
+        if hasattr(fresh, "z_predictor"):
+            out[f"{name}/init/z_bias"] = fresh.z_predictor[-1].bias.detach().numpy().copy()
+        if name == "PoseNetRGBD":
+            for seqn in ("fusion", "rot_head", "trans_head"):
+                for i, layer in enumerate(getattr(fresh, seqn)):
+                    if isinstance(layer, torch.nn.Linear):
+                        w = layer.weight.detach().double()
+                        out[f"{name}/init/{seqn}.{i}/absmax_std"] = np.asarray([w.abs().max().item(),
+                                                                                w.std().item()], np.float64)
+                        out[f"{name}/init/{seqn}.{i}/bias_absmax"] = np.asarray(layer.bias.abs().max().item())
+        # --- seeded parameters for everything outside the trunks -----------------------
+        torch.manual_seed(1)
+        m = classes[name](pretrained=False)
+        shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+        sd = head_weights(shapes, MODEL_WEIGHT_SEED[name])
+        missing, unexpected = m.load_state_dict(sd, strict=False)
+        assert not unexpected and all(k.startswith(("backbone.", "rgb_backbone.", "depth_backbone."))
+                                      or k.endswith("num_batches_tracked") for k in missing), missing
+        out[f"{name}/weights_checksum"] = np.asarray([tensor_checksum(sd[k]) for k in sorted(sd)], np.float64)
+        feats = {}
+
+        def hook(tn):
+            def fn(mod, args, y):
+                feats[tn] = y
+                if y.requires_grad:
+                    y.retain_grad()
+            return fn
+        handles = [getattr(m, tn).register_forward_hook(hook(tn)) for tn in trunks]
+        zf = {}
+        if name == "PoseNetRGBGeometric":
+            def zhook(mod, args, y):
+                zf["z"] = y
+                if y.requires_grad:
+                    y.retain_grad()
+            handles.append(m.z_backbone.register_forward_hook(zhook))
+        args = [inp[a] for a in argnames]
+        # eval mode (running statistics, dropout off)
+        m.eval()
+        with torch.no_grad():
+            rot, trans = m(*args)
+        out[f"{name}/eval/rot"], out[f"{name}/eval/trans"] = rot.numpy(), trans.numpy()
+        for tn in trunks:
+            out[f"{name}/eval/feat/{tn}"] = feats[tn].reshape(MODEL_B, -1).numpy()
+        if zf:
+            out[f"{name}/eval/zfeat"] = zf["z"].numpy()
+        # train mode, Dropout modules in eval (SURVEY.md Appendix A), PoseLoss(1, 10)
+        m.train()
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.Dropout):
+                mod.eval()
+        rot, trans = m(*args)
+        loss = ref_pl.PoseLoss(rot_weight=1.0, trans_weight=10.0, rotation_loss="geodesic")(
+            rot, trans, inp["gt_rot"], inp["gt_trans"])
+        loss.backward()
+        out[f"{name}/train/rot"], out[f"{name}/train/trans"] = rot.detach().numpy(), trans.detach().numpy()
+        out[f"{name}/train/loss"] = np.asarray(loss.item(), np.float64)
+        for tn in trunks:
+            out[f"{name}/train/feat/{tn}"] = feats[tn].detach().reshape(MODEL_B, -1).numpy()
+            out[f"{name}/train/feat_grad/{tn}"] = feats[tn].grad.reshape(MODEL_B, -1).numpy()
+        if zf:
+            out[f"{name}/train/zfeat"] = zf["z"].detach().numpy()
+            out[f"{name}/train/zfeat_grad"] = zf["z"].grad.numpy()
+        _record_grads(out, f"{name}/train", [(k, p) for k, p in m.named_parameters()
+                                             if not k.startswith(("backbone.", "rgb_backbone.", "depth_backbone."))])
+        for k, v in m.state_dict().items():
+            if k.startswith(("backbone.", "rgb_backbone.", "depth_backbone.")):
+                continue
+            if "running" in k or k.endswith("num_batches_tracked"):
+                out[f"{name}/train/state/{k}"] = v.numpy().copy()
+        for h in handles:
+            h.remove()
+    np.savez_compressed(os.path.join(OUT, "models.npz"), **out)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(1)
     ref_pl = _load("ref_pose_loss", "models/pose_loss.py")
     ref_al = _load("ref_add_loss", "models/add_loss.py")
-    gen_pose_loss(ref_pl)
-    gen_add(ref_al)
-    gen_model_parts()
+    only = sys.argv[1:]
+    if not only or "pose_loss" in only:
+        gen_pose_loss(ref_pl)
+    if not only or "add" in only:
+        gen_add(ref_al)
+    if not only or "parts" in only:
+        gen_model_parts()
+    if not only or "models" in only:
+        gen_models(ref_pl)
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 
