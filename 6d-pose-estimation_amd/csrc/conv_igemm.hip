@@ -1454,7 +1454,20 @@ Plan choose(int dtype, int mode, const Geom& g, bool fused = false, const pose6d
     p.g.RH = g.RH / 2;
     p.g.RW = g.RW / 2;
   }
-  const int dflt_tile = pick_tile_fast(dtype, p.g.M, g.Ncols, g.K);
+  // build-time forward-plan overrides (A/B variant builds only: tools/build_variant.sh);
+  // they apply to bf16 forward convs with M <= POSE6D_FWD_OVR_MAXM
+#ifndef POSE6D_FWD_OVR_MAXM
+#define POSE6D_FWD_OVR_MAXM 0
+#endif
+#ifndef POSE6D_FWD_TILE
+#define POSE6D_FWD_TILE -1
+#endif
+#ifndef POSE6D_FWD_STAGES
+#define POSE6D_FWD_STAGES 0
+#endif
+  const bool ovr = fwd && dtype == POSE6D_DT_BF16 && p.g.M <= POSE6D_FWD_OVR_MAXM;
+  int dflt_tile = pick_tile_fast(dtype, p.g.M, g.Ncols, g.K);
+  if (ovr && POSE6D_FWD_TILE >= 0) dflt_tile = POSE6D_FWD_TILE;
   p.tile = (fused || mode == kGemmDual) ? 3 : tune(tn, &pose6d_tuning_t::conv_tile, dflt_tile);
   if (p.tile == 2 || p.tile < 0 || p.tile > 5) p.tile = 3;   // no 64x128 instance on the fast path
   // two slots (32 KiB at 64x64) keep several workgroups per CU resident, which hides
@@ -1469,6 +1482,7 @@ Plan choose(int dtype, int mode, const Geom& g, bool fused = false, const pose6d
   // fp32 forward (MFMA-bound: 4 exact 16x16x4 MFMAs per 16-byte chunk): 3 slots for
   // 1x1 filters, 2 for the rest (tools/conv_bench.py --graph --dtype f32 sweep, round 2)
   if (dtype == POSE6D_DT_F32 && (p.mode == kGemm || p.mode == kFwd)) dflt = (g.KH == 1 && g.KW == 1) ? 3 : 2;
+  if (ovr && POSE6D_FWD_STAGES > 0) dflt = POSE6D_FWD_STAGES;
   p.stages = tune(tn, &pose6d_tuning_t::conv_stages, dflt);
   if (p.stages < 2) p.stages = 2;
   if (p.stages > 6) p.stages = 6;

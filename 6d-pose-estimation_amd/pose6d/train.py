@@ -71,7 +71,7 @@ class RGBDGeometricTrainer:
 
     def __init__(self, model, batch, dtype=torch.bfloat16, lr=1e-4, weight_decay=1e-4, max_norm=1.0,
                  betas=(0.9, 0.999), eps=1e-8, rot_weight=1.0, trans_weight=10.0, process_group=None,
-                 bucket_mb=25.0, tail_mb=2.0):
+                 bucket_mb=25.0, tail_mb=2.0, force_buckets=False):
         self.model = model
         self.B = batch
         dev = next(model.parameters()).device
@@ -88,6 +88,10 @@ class RGBDGeometricTrainer:
         self.m = torch.zeros_like(self.arena.flat)
         self.v = torch.zeros_like(self.arena.flat)
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        # the bucketed all-reduce path (segmented graphs, comm stream, async collectives):
+        # every world > 1, and world 1 with force_buckets (exercises the RCCL branch on a
+        # one-GPU box: an all-reduce over one rank returns its input)
+        self._ddp = process_group is not None and (self.world > 1 or force_buckets)
         # hp[6]: gradient scale read by adamw_step -- 1/world averages the all-reduced sum
         # inside the update (exact for power-of-two world sizes: scaling by 2^-k commutes
         # with every rounding; arena.grad then holds the SUM after a step).  Other world
@@ -122,7 +126,7 @@ class RGBDGeometricTrainer:
         (stem / layer1, ready only when the backward ends: its all-reduce is not
         overlapped) is capped at tail_mb (tools/ddp_overlap.py models the tail)."""
         self.bucket_ends = []
-        if self.world == 1:
+        if not self._ddp:
             return
         sizes = [(off, p.numel()) for p, off in zip(self.arena.params, self.arena.offsets)]
         ends = plan_buckets(sizes, int(bucket_mb * 1e6 / 4), int(tail_mb * 1e6 / 4))
@@ -159,7 +163,7 @@ class RGBDGeometricTrainer:
 
     def step_eager(self, data):
         """One training step without graphs (reference order of operations)."""
-        if self.world == 1:
+        if not self._ddp:
             return self.step_body(data)
         self.trunk.pack_weights(force=True)
         self._forward_loss(*data)
@@ -209,7 +213,7 @@ class RGBDGeometricTrainer:
                 self.step_eager(data)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        if self.world == 1:
+        if not self._ddp:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self.step_body(data)
@@ -267,7 +271,7 @@ class RGBDGeometricTrainer:
     def step(self, data=None):
         if self.graphs is None:
             return self.step_eager(data)
-        if self.world == 1:
+        if not self._ddp:
             self.graphs[0].replay()
             return
         red = self._red

@@ -1,0 +1,72 @@
+"""Worker of tests/test_ddp_gpu.py::test_rccl_world1_bucketed_step (torch.distributed.run
+--nproc-per-node 1): ONE rank over RCCL (backend 'nccl', device_id bound) driving the
+data-parallel machinery bench.py --gpus N uses on an 8-GPU node -- the 25 MB gradient
+buckets, the comm stream, async all-reduce handles around the segmented-graph replay
+(RGBDGeometricTrainer(force_buckets=True)) -- at bs32 bf16 (BASELINE configs[4] per rank).
+An all-reduce over one rank returns its input, so eager and replayed steps must equal
+the plain world-1 step bit for bit (parameters, AdamW moments, BN running statistics).
+argv: OUT"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "6d-pose-estimation_amd")]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def main():
+    out = sys.argv[1]
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist.init_process_group("nccl", device_id=dev)
+    assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+    from bench import synth_batch
+    from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
+    from pose6d.train import RGBDGeometricTrainer
+    B = 32
+    data = synth_batch(B, dev, seed=1000)
+
+    def trainer(pg):
+        torch.manual_seed(0)
+        model = PoseNetRGBDGeometric(pretrained=False).to(dev)
+        for m in model.modules():
+            if isinstance(m, torch.nn.Dropout):
+                m.eval()
+        return RGBDGeometricTrainer(model, B, dtype=torch.bfloat16, process_group=pg, force_buckets=pg is not None)
+
+    def state(tr):
+        bufs = [v.float().flatten() for k, v in tr.model.state_dict().items() if "running" in k]
+        return torch.cat([tr.arena.flat, tr.m, tr.v] + bufs)
+
+    ref = trainer(None)
+    ref.step_eager(data)
+    ref.step_eager(data)
+    torch.cuda.synchronize()
+    want = state(ref)
+    # eager bucketed steps: comm stream + async RCCL all-reduces overlapping backward
+    tr = trainer(dist.group.WORLD)
+    n_buckets = len(tr.bucket_ends)
+    tr.step_eager(data)
+    tr.step_eager(data)
+    torch.cuda.synchronize()
+    eager_same = torch.equal(state(tr), want)
+    # segmented graphs replayed with the all-reduces between the replays
+    trg = trainer(dist.group.WORLD)
+    snap = trg.snapshot()
+    trg.capture(data)
+    trg.restore(snap)
+    trg.step()
+    trg.step()
+    torch.cuda.synchronize()
+    graph_same = torch.equal(state(trg), want)
+    n_segs = len(trg.graphs) - 1
+    with open(out, "w") as f:
+        f.write(f"{int(eager_same)} {int(graph_same)} {n_buckets} {n_segs} {dist.get_backend()}\n")
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

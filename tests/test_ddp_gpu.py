@@ -55,3 +55,24 @@ def test_bench_world2_json_line():
     assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 64 and res["config"]["per_gpu_batch"] == 32
     assert res["config"]["parallelism"] == "dp2" and res["scaling"] == "weak"
     assert res["value"] > 0 and abs(res["value"] - 64 * 1e3 / res["ms_per_step"]) < 1e-3 * res["value"] + 0.1
+
+
+@pytest.mark.gpu
+def test_rccl_world1_bucketed_step():
+    """The RCCL branch itself (backend 'nccl' with device_id, as bench.py initialises it
+    for N > 1): one rank under torch.distributed.run, the trainer forced onto the
+    bucketed path (25 MB buckets, comm stream, async all-reduce handles around the
+    segmented-graph replay).  A one-rank all-reduce returns its input, so two eager and
+    two replayed steps equal the plain one-GPU steps bit for bit.  Scaling over xGMI
+    stays unmeasured here (one GPU per box)."""
+    out = os.path.join(tempfile.mkdtemp(), "rccl")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", "29691", os.path.join(REPO, "tests", "rccl_worker.py"), out]
+    r = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    eager_same, graph_same, nb, nsegs, backend = open(out).read().split()
+    assert backend == "nccl"
+    assert int(nb) >= 4 and int(nsegs) >= 3, "expected several 25 MB buckets and graph segments"
+    assert eager_same == "1", "eager bucketed RCCL step != plain one-GPU step"
+    assert graph_same == "1", "segmented-graph RCCL step != plain one-GPU step"
