@@ -1151,6 +1151,8 @@ __global__ __launch_bounds__(64 * NW) void conv_lds_kernel(const T* __restrict__
   conv_lds_body<T, BM, BN, MODE, S, ACT, NW, BNR>(smem, blockIdx.x, src, wts, bias, res, out, stats, g);
 }
 
+#include "conv_patch.h"
+
 // Fused backward of one conv.  Both passes read the same dY, and the weight-
 // gradient workgroups fill the CUs the (often small) data-gradient grid leaves idle
 // -- one launch instead of two.  Workgroup order = the order the dispatcher starts
@@ -1467,6 +1469,19 @@ Plan choose(int dtype, int mode, const Geom& g, bool fused = false, const pose6d
 #endif
   const bool ovr = fwd && dtype == POSE6D_DT_BF16 && p.g.M <= POSE6D_FWD_OVR_MAXM;
   int dflt_tile = pick_tile_fast(dtype, p.g.M, g.Ncols, g.K);
+  // long-K 1x1 forwards on the small grids (layer3 / layer4 at batch 32, M <= 6272): 8-wave
+  // tiles on a 4-slot ring -- 128x128 where that still gives >= 96 workgroups, else
+  // 128x64.  In-graph eval times (profiles/r05b_eval_variants.txt): 1024->256 16.0 ->
+  // 11.0 us, 1024->512 18.9 -> 15.9, 1024->2048/s2 17.5 -> 15.2, 2048->512 12.9 -> 12.3
+#ifndef POSE6D_LONG1X1
+#define POSE6D_LONG1X1 1   // build-time (A/B): 0 = the round-4 tile / ring rules for these convs
+#endif
+  const bool long1x1 = POSE6D_LONG1X1 && fwd && dtype == POSE6D_DT_BF16 && g.KH == 1 && g.KW == 1 && g.K >= 1024 &&
+                       p.g.M <= 6272;
+  if (long1x1) {
+    const int64_t wg4 = (int64_t)p6::ceil_div(p.g.M, 128) * p6::ceil_div(g.Ncols, 128);
+    dflt_tile = (g.Ncols >= 512 && wg4 >= 96) ? 4 : 5;
+  }
   if (ovr && POSE6D_FWD_TILE >= 0) dflt_tile = POSE6D_FWD_TILE;
   p.tile = (fused || mode == kGemmDual) ? 3 : tune(tn, &pose6d_tuning_t::conv_tile, dflt_tile);
   if (p.tile == 2 || p.tile < 0 || p.tile > 5) p.tile = 3;   // no 64x128 instance on the fast path
@@ -1482,6 +1497,7 @@ Plan choose(int dtype, int mode, const Geom& g, bool fused = false, const pose6d
   // fp32 forward (MFMA-bound: 4 exact 16x16x4 MFMAs per 16-byte chunk): 3 slots for
   // 1x1 filters, 2 for the rest (tools/conv_bench.py --graph --dtype f32 sweep, round 2)
   if (dtype == POSE6D_DT_F32 && (p.mode == kGemm || p.mode == kFwd)) dflt = (g.KH == 1 && g.KW == 1) ? 3 : 2;
+  if (long1x1) dflt = 4;
   if (ovr && POSE6D_FWD_STAGES > 0) dflt = POSE6D_FWD_STAGES;
   p.stages = tune(tn, &pose6d_tuning_t::conv_stages, dflt);
   if (p.stages < 2) p.stages = 2;
@@ -1504,6 +1520,28 @@ Plan choose(int dtype, int mode, const Geom& g, bool fused = false, const pose6d
   if (p.g.splits > 1 && tune(tn, &pose6d_tuning_t::conv_stages, -1) < 0 && p.stages < 4 && !(cols128 && rows128))
     p.stages = 4;
   return p;
+}
+
+#ifndef POSE6D_PATCH
+#define POSE6D_PATCH 1   // build-time (A/B): 0 = 3x3 forwards always on the implicit GEMM
+#endif
+constexpr int kPatchStages = 4;
+// the patch plan applies to bf16 3x3 / stride 1 / pad 1 forwards with 64-channel
+// slices and no BatchNorm statistics, unless a tuning forces an implicit-GEMM plan
+// (tile / ring / kernel / split-K) or turns it off (conv_patch = 0)
+bool patch_eligible(int dtype, int mode, const Geom& g, const float* stats, const pose6d_tuning_t* tn,
+                    PatchPlan* pp) {
+  if (!POSE6D_PATCH || dtype != POSE6D_DT_BF16 || mode != kFwd || stats != nullptr) return false;
+  if (g.KH != 3 || g.KW != 3 || g.stride != 1 || g.pad != 1 || g.SH != g.RH || g.SW != g.RW) return false;
+  if (g.SC % 64 != 0 || g.Ncols % kPatchBN != 0 || g.Kpad != g.K || g.act_rscale != nullptr) return false;
+  if (tn) {
+    if (tn->conv_patch == 0) return false;
+    if (tn->conv_patch < 0 && (tn->conv_tile >= 0 || tn->conv_stages >= 0 || tn->conv_base >= 0 ||
+                               tn->conv_splitk >= 0))
+      return false;
+  }
+  *pp = patch_plan(g.M / (g.RH * g.RW), g.RH, g.RW, g.SC, g.Ncols, kPatchStages);
+  return pp->ok;
 }
 
 // bytes of split-K workspace a plan needs (0: it does not split K)
@@ -1529,6 +1567,13 @@ int run_conv(int dtype, int mode, const Geom& g, const void* src, const void* w,
     P6_CHECK_ARG(((uintptr_t)sk_ws & 255) == 0, "conv: the split-K workspace must be 256-byte aligned");
     p.g.sk_cnt = (int*)sk_ws;
     p.g.sk_part = (float*)((char*)sk_ws + kSkCntBytes);
+  }
+  // 3x3 stride-1 bf16 forwards without BatchNorm statistics (eval; conv_patch.h): the
+  // input patch staged once per 64-channel slice instead of once per filter tap
+  {
+    PatchPlan pp{};
+    if (patch_eligible(dtype, mode, g, stats, tn, &pp))
+      return launch_patch<kPatchStages>(g, pp, g.M / (g.RH * g.RW), src, w, bias, res, out, s);
   }
   if (p.fast) return dispatch_fast(dtype, p.mode, p.g, p.tile, p.stages, src, w, bias, res, out, stats, s);
   return dtype == POSE6D_DT_BF16 ? dispatch<bf16>(mode, g, p.tile, src, w, bias, res, out, stats, s)
@@ -1956,6 +2001,16 @@ extern "C" int pose6d_conv_variant(int32_t dtype, int32_t pass, int32_t N, int32
                            : dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
   const Plan p = choose(dtype, mode, g, false, nullptr, pass == 0);
   return (p.g.splits << 16) | (p.stages << 12) | ((int)p.fast << 8) | (p.mode << 4) | p.tile;
+}
+
+// workgroups of the patch plan a stats-free forward of this geometry runs (0 = the
+// implicit-GEMM plans of pose6d_conv_variant)
+extern "C" int pose6d_conv_patch_plan(int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout,
+                                      int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo) {
+  int mode;
+  const Geom g = fwd_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
+  PatchPlan pp{};
+  return patch_eligible(dtype, mode, g, nullptr, nullptr, &pp) ? pp.tiles * (Cout / kPatchBN) : 0;
 }
 
 // split-K workspace bytes of a forward (pass 0) / data-gradient (pass 1) conv's plan:

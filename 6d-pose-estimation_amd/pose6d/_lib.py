@@ -81,7 +81,7 @@ class Tuning(ctypes.Structure):
     entry points' *_tuned forms (tests / tuning tools only; -1 = default)."""
     _fields_ = [(n, ctypes.c_int32) for n in ("conv_tile", "conv_stages", "conv_s2", "conv_base", "wgrad_stages",
                                                "wgrad_base", "bwd_separate", "conv_splitk", "wgrad_splits",
-                                               "bwd_order")]
+                                               "bwd_order", "conv_patch")]
 
     def __init__(self, **kw):
         super().__init__(*([-1] * len(self._fields_)))

@@ -216,6 +216,13 @@ int64_t pose6d_conv_splitk_workspace(int32_t dtype, int32_t pass, int32_t N, int
 int pose6d_conv_variant(int32_t dtype, int32_t pass, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout,
                         int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo);
 int pose6d_wgrad_variant(int32_t dtype, int32_t M, int32_t Cout, int32_t K, int32_t Cin);
+/* 3x3 / stride 1 / pad 1 bf16 forwards WITHOUT BatchNorm statistics (eval: pose6d_conv2d_fwd
+ * with stats == NULL, pose6d_conv2d_fwd_act) on >= 64-channel slices run the patch kernel
+ * (conv3x3_patch_kernel: each workgroup stages its input patch once per 64-channel slice
+ * instead of once per filter tap): its workgroup count, or 0 when the geometry takes the
+ * implicit-GEMM plans pose6d_conv_variant describes. */
+int pose6d_conv_patch_plan(int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH,
+                           int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo);
 /* eval-mode forward with the BatchNorm folded into the store: out = act(T(conv(x) [+ bias]) * scale + shift
  * [+ res | + res * res_scale + res_shift]), act = ReLU if relu -- pose6d_conv2d_fwd followed by
  * pose6d_bn_act_fwd bit for bit, one launch, no raw-output round trip.  res: NHWC like out (or NULL). */
@@ -277,11 +284,14 @@ int pose6d_conv2d_backward(int32_t dtype, const void *x, const void *dy, const v
  *                 split over this many workgroups of one launch (1 = none)
  *   wgrad_splits  weight gradient: pixel splits (slabs) of the plan (>= 1; tools only)
  *   bwd_order     fused backward: 1 = weight-gradient workgroups dispatched first, 0 = data gradient first
+ *   conv_patch    3x3 stride-1 bf16 forwards without BatchNorm statistics: 0 = the implicit-GEMM plan,
+ *                 1 or -1 = the patch plan (-1 only while no conv_tile / conv_stages / conv_base /
+ *                 conv_splitk is forced)
  * A tuned plan that splits K needs pose6d_conv_splitk_workspace_tuned(...) bytes of
  * split-K workspace (see pose6d_conv_splitk_workspace). */
 typedef struct {
   int32_t conv_tile, conv_stages, conv_s2, conv_base, wgrad_stages, wgrad_base, bwd_separate, conv_splitk;
-  int32_t wgrad_splits, bwd_order;
+  int32_t wgrad_splits, bwd_order, conv_patch;
 } pose6d_tuning_t;
 int64_t pose6d_conv_splitk_workspace_tuned(int32_t dtype, int32_t pass, int32_t N, int32_t H, int32_t W,
                                            int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,

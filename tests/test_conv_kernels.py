@@ -149,7 +149,7 @@ def test_conv_fast_variants_bit_identical(cfg):
                      device=dev)
 
     def run(tn=None):
-        tn = tn if tn is not None else Tuning()
+        tn = tn if tn is not None else Tuning(conv_patch=0)
         y = torch.empty(N, Ho, Wo, Cout, device=dev, dtype=dtype)
         dx = torch.empty(N, H, W, Cin, device=dev, dtype=dtype)
         dw = torch.empty(Cout, Cin, k, k, device=dev)
@@ -163,16 +163,20 @@ def test_conv_fast_variants_bit_identical(cfg):
         return y.cpu(), dx.cpu(), dw.cpu()
 
     y0, dx0, dw0 = run()
-    # the plain (untuned) entry points are the default plan
+    # the plain (untuned) entry points are the default plan (a stats-free 3x3 stride-1
+    # forward takes the patch kernel: its own K order, compared in test_conv3x3_patch)
     y = torch.empty(N, Ho, Wo, Cout, device=dev, dtype=dtype)
     call("conv2d_fwd", dt, x, wp, None, y, None, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, *skws(), stream())
     torch.cuda.synchronize()
-    assert torch.equal(y.cpu(), y0)
+    if query("conv_patch_plan", dt, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo) == 0:
+        assert torch.equal(y.cpu(), y0)
+    else:
+        _close(y.cpu(), y0, 2e-2, "patch plan vs implicit GEMM")
     variants = [dict(conv_stages=st, conv_tile=t) for st in (2, 3, 4, 6) for t in (0, 1, 3, 4, 5)]
     variants.append(dict(conv_s2=0))
     variants += [dict(wgrad_stages=st) for st in (2, 3, 4)]
     for kw in variants:
-        y1, dx1, dw1 = run(Tuning(**kw))
+        y1, dx1, dw1 = run(Tuning(conv_patch=0, **kw))
         assert torch.equal(y0, y1), f"fwd differs under {kw}"
         assert torch.equal(dx0, dx1), f"dgrad differs under {kw}"
         assert torch.equal(dw0, dw1), f"wgrad differs under {kw}"
@@ -203,6 +207,69 @@ def test_conv_fast_variants_bit_identical(cfg):
     yb, dxb, _ = run(Tuning(conv_base=1))
     _close(yb, y0, 2e-2, "fwd base vs LDS-DMA")
     _close(dxb, dx0, 2e-2, "dgrad base vs LDS-DMA")
+
+
+PATCH_CONFIGS = [
+    # N, H, W, Cin, Cout: tiles of R full rows (14x14: 9 + 5, 28x28: 4, 56x56: 2) or of
+    # whole images (7x7: 2 per tile; odd N leaves a one-image tile)
+    (32, 14, 14, 256, 256),
+    (3, 7, 7, 512, 512),
+    (2, 28, 28, 128, 128),
+    (2, 56, 56, 64, 64),
+    (2, 14, 14, 64, 192),
+    (1, 5, 9, 128, 64),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", PATCH_CONFIGS)
+def test_conv3x3_patch(cfg):
+    """The 3x3 / stride-1 patch kernel (stats-free bf16 forwards): against the torch fp32
+    conv of the same bf16 operands; its eval BN-act epilogue (pose6d_conv2d_fwd_act) bit
+    for bit the plain store + pose6d_bn_act_fwd; close to the implicit-GEMM plan
+    (conv_patch = 0, another K order); a repeated launch reproduces its bits."""
+    from pose6d._lib import Tuning, call, query, stream
+    from pose6d.trunk import DTYPES, pack_single
+    N, H, W, Cin, Cout = cfg
+    dtype = torch.bfloat16
+    dt = DTYPES[dtype]
+    g = torch.Generator().manual_seed(N * 1000 + H * 10 + Cin)
+    x = torch.randn(N, Cin, H, W, generator=g).bfloat16().float()
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) * (2.0 / (Cin * 9)) ** 0.5).bfloat16().float()
+    b = torch.randn(Cout, generator=g) * 0.1
+    assert query("conv_patch_plan", dt, N, H, W, Cin, Cout, 3, 3, 1, 1, H, W) > 0
+    xd = _nhwc(x).to("cuda", dtype)
+    wp, _ = pack_single(w.cuda(), Cin, dtype, with_t=False)
+    bd = b.cuda()
+
+    def fwd(tn=None, bias=None):
+        y = torch.empty(N, H, W, Cout, device="cuda", dtype=dtype)
+        if tn is None:
+            call("conv2d_fwd", dt, xd, wp, bias, y, None, N, H, W, Cin, Cout, 3, 3, 1, 1, H, W, *skws(), stream())
+        else:
+            call("conv2d_fwd_tuned", dt, xd, wp, bias, y, None, N, H, W, Cin, Cout, 3, 3, 1, 1, H, W, tn.ref,
+                 *skws(), stream())
+        torch.cuda.synchronize()
+        return y.cpu()
+
+    y = fwd()
+    ref = F.conv2d(x, w, None, stride=1, padding=1)
+    _close(y.permute(0, 3, 1, 2), ref, 2e-2, "patch fwd")
+    assert torch.equal(fwd(), y), "repeated launch differs"
+    yb = fwd(bias=bd)
+    _close(yb.permute(0, 3, 1, 2), ref + b.view(1, -1, 1, 1), 2e-2, "patch fwd + bias")
+    yg = fwd(Tuning(conv_patch=0))
+    _close(yg, y, 2e-2, "implicit GEMM vs patch")
+    # eval BN-act epilogue == plain store + pose6d_bn_act_fwd, bit for bit
+    sc = (torch.rand(Cout, generator=g) + 0.5).cuda()
+    sh = (torch.randn(Cout, generator=g) * 0.1).cuda()
+    fused = torch.empty(N, H, W, Cout, device="cuda", dtype=dtype)
+    call("conv2d_fwd_act", dt, xd, wp, bd, fused, N, H, W, Cin, Cout, 3, 3, 1, 1, H, W, sc, sh, None, None, None, 1,
+         *skws(), stream())
+    sep = torch.empty(N, H, W, Cout, device="cuda", dtype=dtype)
+    call("bn_act_fwd", dt, yb.cuda(), sc, sh, None, None, None, 1, sep, N * H * W, Cout, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(fused.cpu(), sep.cpu()), "patch BN-act epilogue != conv + bn_act"
 
 
 SPLITK_CONFIGS = [
