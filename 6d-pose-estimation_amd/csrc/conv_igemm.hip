@@ -985,8 +985,11 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
     }
   };
 
-  auto issue = [&](int kt, int buf) {
-    (void)kt;
+  // one stage's DMA as (source, LDS destination) pairs, then the tap walk advanced;
+  // issue() fires them back to back, the interleaved compute (POSE6D_ILV) one per MFMA
+  const T* dsrc[LOADS];
+  char* ddst[LOADS];
+  auto prep = [&](int buf) {
     char* As = smem + buf * STAGE;
     char* Bs = As + SA;
     if (c0 == 0) set_tap();
@@ -995,10 +998,14 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
     for (int j = 0; j < B_INS; ++j) {
       const T* bb = b_base[j];
       if constexpr (DUAL) bb = phase ? b_base2[j] : b_base[j];
-      glds16(bb + (boff & b_mask[j]), Bs + (j * RW + wave * 8) * 128);
+      dsrc[j] = bb + (boff & b_mask[j]);
+      ddst[j] = Bs + (j * RW + wave * 8) * 128;
     }
 #pragma unroll
-    for (int i = 0; i < A_INS; ++i) glds16(a_base[i] + ((unsigned)c0 & a_mask[i]), As + (i * RW + wave * 8) * 128);
+    for (int i = 0; i < A_INS; ++i) {
+      dsrc[B_INS + i] = a_base[i] + ((unsigned)c0 & a_mask[i]);
+      ddst[B_INS + i] = As + (i * RW + wave * 8) * 128;
+    }
     c0 += KS;
     if (c0 == tap_len) {
       c0 = 0;
@@ -1016,6 +1023,12 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
         tap_koff += g.SC;
       }
     }
+  };
+  auto issue = [&](int kt, int buf) {
+    (void)kt;
+    prep(buf);
+#pragma unroll
+    for (int q = 0; q < LOADS; ++q) glds16(dsrc[q], ddst[q]);
   };
 
   // split-K: this workgroup's K-steps [kb, ke) of the tile; the tap walk starts at kb
@@ -1061,6 +1074,57 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   const unsigned ring_base = lds_addr(smem);
   // mid(): issued between the fragment reads and their wait, so the next stage's
   // LDS-DMA issue (tens of cycles per instruction) overlaps the LDS read latency
+  // POSE6D_ILV: the next stage's DMA instructions issued one after each first-k-half
+  // MFMA instead of as one burst before them (a DMA wave-instruction costs the wave
+  // ~60-185 issue cycles, an MFMA 16 of pipe time: interleaved, the issue cost hides
+  // behind the matrix pipe)
+  auto compute_ilv = [&](int buf, bool has, auto& acc) {
+    const unsigned slot = ring_base + buf * STAGE;
+    constexpr int NM = TM * TN;   // MFMAs per k-half
+    constexpr int GAP = NM / LOADS > 0 ? NM / LOADS : 1;
+    if constexpr (TM + TN == 4 && kPairedFrags) {
+      unsigned addr[2][4];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) addr[kk][r] = slot + frag_off[kk][r];
+      u32x4 f[2][4];
+      lds_issue_frags8(f, addr);
+      lds_wait_first(f[0]);
+#pragma unroll
+      for (int q = 0; q < NM; ++q) {
+        mma_frag<T>(acc[q / TN][q % TN], f[0][q / TN], f[0][TM + q % TN]);
+        if (q % GAP == GAP - 1 && q / GAP < LOADS && has) glds16(dsrc[q / GAP], ddst[q / GAP]);
+      }
+#pragma unroll
+      for (int q = NM / GAP; q < LOADS; ++q)
+        if (has) glds16(dsrc[q], ddst[q]);
+      lds_wait_all(f[1]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) mma_frag<T>(acc[i][j], f[1][i], f[1][TM + j]);
+      return;
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      unsigned addr[TM + TN];
+#pragma unroll
+      for (int r = 0; r < TM + TN; ++r) addr[r] = slot + frag_off[kk][r];
+      u32x4 f[TM + TN];
+      lds_read_frags<TM + TN>(f, addr);
+#pragma unroll
+      for (int q = 0; q < NM; ++q) {
+        mma_frag<T>(acc[q / TN][q % TN], f[q / TN], f[TM + q % TN]);
+        if (kk == 0 && q % GAP == GAP - 1 && q / GAP < LOADS && has) glds16(dsrc[q / GAP], ddst[q / GAP]);
+      }
+      if (kk == 0) {
+#pragma unroll
+        for (int q = NM / GAP; q < LOADS; ++q)
+          if (has) glds16(dsrc[q], ddst[q]);
+      }
+    }
+  };
   auto compute = [&](int buf, auto&& mid, auto& acc) {
     const unsigned slot = ring_base + buf * STAGE;
     if constexpr (TM + TN == 4 && kPairedFrags) {
@@ -1126,7 +1190,16 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
           }
       }
     }
-    compute(cur, mid, acc);
+#ifndef POSE6D_ILV
+#define POSE6D_ILV 0
+#endif
+    if constexpr (POSE6D_ILV && !DUAL) {
+      const bool has = kt + S - 1 < nk;
+      if (has) prep(wbuf);
+      compute_ilv(cur, has, acc);
+    } else {
+      compute(cur, mid, acc);
+    }
     cur = cur == S - 1 ? 0 : cur + 1;
     wbuf = wbuf == S - 1 ? 0 : wbuf + 1;
   }
@@ -1525,7 +1598,9 @@ Plan choose(int dtype, int mode, const Geom& g, bool fused = false, const pose6d
 #ifndef POSE6D_PATCH
 #define POSE6D_PATCH 1   // build-time (A/B): 0 = 3x3 forwards always on the implicit GEMM
 #endif
-constexpr int kPatchStages = 4;
+// 2 ring slots: deeper rings measured slower (graph-timed, profiles/r05d_patch_sweep.txt:
+// 56x56 64->64 17.8 / 23.5 / 25.1 us at 2 / 3 / 6 slots)
+constexpr int kPatchStages = 2;
 // the patch plan applies to bf16 3x3 / stride 1 / pad 1 forwards with 64-channel
 // slices and no BatchNorm statistics, unless a tuning forces an implicit-GEMM plan
 // (tile / ring / kernel / split-K) or turns it off (conv_patch = 0)
@@ -1539,7 +1614,13 @@ bool patch_eligible(int dtype, int mode, const Geom& g, const float* stats, cons
     if (tn->conv_patch < 0 && (tn->conv_tile >= 0 || tn->conv_stages >= 0 || tn->conv_base >= 0 ||
                                tn->conv_splitk >= 0))
       return false;
+    if (tn->conv_patch == 1 && (tn->conv_tile >= 0 || tn->conv_base >= 0 || tn->conv_splitk >= 0))
+      return false;
   }
+  // the 28x28 and 56x56 stages only: on 14x14 / 7x7 (few tiles per image, long K) the
+  // implicit GEMM is as fast or faster (profiles/r05d_patch_sweep.txt: 17.7 vs 18.3 us,
+  // 19.1 vs 48.2 us)
+  if (g.RH * g.RW < 784 && !(tn && tn->conv_patch == 1)) return false;
   *pp = patch_plan(g.M / (g.RH * g.RW), g.RH, g.RW, g.SC, g.Ncols, kPatchStages);
   return pp->ok;
 }
@@ -1572,8 +1653,19 @@ int run_conv(int dtype, int mode, const Geom& g, const void* src, const void* w,
   // input patch staged once per 64-channel slice instead of once per filter tap
   {
     PatchPlan pp{};
-    if (patch_eligible(dtype, mode, g, stats, tn, &pp))
-      return launch_patch<kPatchStages>(g, pp, g.M / (g.RH * g.RW), src, w, bias, res, out, s);
+    if (patch_eligible(dtype, mode, g, stats, tn, &pp)) {
+      const int st = tn && tn->conv_patch == 1 && tn->conv_stages > 0 ? tn->conv_stages : kPatchStages;
+      if (st != kPatchStages) pp = patch_plan(g.M / (g.RH * g.RW), g.RH, g.RW, g.SC, g.Ncols, st);
+      P6_CHECK_ARG(pp.ok, "conv: patch plan with %d ring slots exceeds the LDS", st);
+      const int N = g.M / (g.RH * g.RW);
+      switch (st) {
+        case 3: return launch_patch<3>(g, pp, N, src, w, bias, res, out, s);
+        case 4: return launch_patch<4>(g, pp, N, src, w, bias, res, out, s);
+        case 6: return launch_patch<6>(g, pp, N, src, w, bias, res, out, s);
+        case 8: return launch_patch<8>(g, pp, N, src, w, bias, res, out, s);
+        default: return launch_patch<kPatchStages>(g, pp, N, src, w, bias, res, out, s);
+      }
+    }
   }
   if (p.fast) return dispatch_fast(dtype, p.mode, p.g, p.tile, p.stages, src, w, bias, res, out, stats, s);
   return dtype == POSE6D_DT_BF16 ? dispatch<bf16>(mode, g, p.tile, src, w, bias, res, out, stats, s)

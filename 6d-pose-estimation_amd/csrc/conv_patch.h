@@ -90,7 +90,40 @@ __device__ __forceinline__ void vm_wait_barrier(int n) {
     case 12: vmcnt_barrier<12>(); break;
     case 13: vmcnt_barrier<13>(); break;
     case 14: vmcnt_barrier<14>(); break;
-    default: vmcnt_barrier<15>(); break;
+    case 15: vmcnt_barrier<15>(); break;
+    case 16: vmcnt_barrier<16>(); break;
+    case 17: vmcnt_barrier<17>(); break;
+    case 18: vmcnt_barrier<18>(); break;
+    case 19: vmcnt_barrier<19>(); break;
+    case 20: vmcnt_barrier<20>(); break;
+    case 21: vmcnt_barrier<21>(); break;
+    case 22: vmcnt_barrier<22>(); break;
+    case 23: vmcnt_barrier<23>(); break;
+    case 24: vmcnt_barrier<24>(); break;
+    case 25: vmcnt_barrier<25>(); break;
+    case 26: vmcnt_barrier<26>(); break;
+    case 27: vmcnt_barrier<27>(); break;
+    case 28: vmcnt_barrier<28>(); break;
+    case 29: vmcnt_barrier<29>(); break;
+    case 30: vmcnt_barrier<30>(); break;
+    case 31: vmcnt_barrier<31>(); break;
+    case 32: vmcnt_barrier<32>(); break;
+    case 33: vmcnt_barrier<33>(); break;
+    case 34: vmcnt_barrier<34>(); break;
+    case 35: vmcnt_barrier<35>(); break;
+    case 36: vmcnt_barrier<36>(); break;
+    case 37: vmcnt_barrier<37>(); break;
+    case 38: vmcnt_barrier<38>(); break;
+    case 39: vmcnt_barrier<39>(); break;
+    case 40: vmcnt_barrier<40>(); break;
+    case 41: vmcnt_barrier<41>(); break;
+    case 42: vmcnt_barrier<42>(); break;
+    case 43: vmcnt_barrier<43>(); break;
+    case 44: vmcnt_barrier<44>(); break;
+    case 45: vmcnt_barrier<45>(); break;
+    case 46: vmcnt_barrier<46>(); break;
+    case 47: vmcnt_barrier<47>(); break;
+    default: vmcnt_barrier<0>(); break;
   }
 }
 

@@ -113,6 +113,9 @@ def main():
         fns = {
             "fwd": lambda: call("conv2d_fwd_tuned", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k, k, s, p, Ho,
                                 Wo, TUNE.ref, skw, skw.numel(), stream()),
+            # tuned, no BN statistics (stats-free plans: the 3x3 patch kernel)
+            "fwdnst": lambda: call("conv2d_fwd_tuned", dt, x, wp, None, y, None, B, H, W, Cin, Cout, k, k, s, p, Ho,
+                                   Wo, TUNE.ref, skw, skw.numel(), stream()),
             # no BN statistics (as in eval without the fold)
             "fwdns": lambda: call("conv2d_fwd", dt, x, wp, None, y, None, B, H, W, Cin, Cout, k, k, s, p, Ho, Wo,
                                   skw, skw.numel(), stream()),
