@@ -1617,10 +1617,11 @@ bool patch_eligible(int dtype, int mode, const Geom& g, const float* stats, cons
     if (tn->conv_patch == 1 && (tn->conv_tile >= 0 || tn->conv_base >= 0 || tn->conv_splitk >= 0))
       return false;
   }
-  // the 28x28 and 56x56 stages only: on 14x14 / 7x7 (few tiles per image, long K) the
-  // implicit GEMM is as fast or faster (profiles/r05d_patch_sweep.txt: 17.7 vs 18.3 us,
-  // 19.1 vs 48.2 us)
-  if (g.RH * g.RW < 784 && !(tn && tn->conv_patch == 1)) return false;
+  // the 56x56 stage only: in the eval graph the layer1 3x3 convs gain 1.7-2.5 us each,
+  // the 28x28 ones lose 0.5-0.7 us (profiles/r05e_eval_layers.txt), and on 14x14 / 7x7
+  // (few tiles per image, long K) the implicit GEMM is faster (profiles/r05d_patch_sweep.txt:
+  // 17.7 vs 18.3 us, 19.1 vs 48.2 us)
+  if (g.RH * g.RW < 3136 && !(tn && tn->conv_patch == 1)) return false;
   *pp = patch_plan(g.M / (g.RH * g.RW), g.RH, g.RW, g.SC, g.Ncols, kPatchStages);
   return pp->ok;
 }

@@ -224,10 +224,12 @@ PATCH_CONFIGS = [
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", PATCH_CONFIGS)
 def test_conv3x3_patch(cfg):
-    """The 3x3 / stride-1 patch kernel (stats-free bf16 forwards): against the torch fp32
-    conv of the same bf16 operands; its eval BN-act epilogue (pose6d_conv2d_fwd_act) bit
-    for bit the plain store + pose6d_bn_act_fwd; close to the implicit-GEMM plan
-    (conv_patch = 0, another K order); a repeated launch reproduces its bits."""
+    """The 3x3 / stride-1 patch kernel (stats-free bf16 forwards; the default plan on the
+    56x56 stage, forced with conv_patch = 1 elsewhere): against the torch fp32
+    conv of the same bf16 operands; close to the implicit-GEMM plan (conv_patch = 0,
+    another K order); a repeated launch reproduces its bits; the untuned eval BN-act
+    epilogue (pose6d_conv2d_fwd_act) is bit for bit the untuned plain store +
+    pose6d_bn_act_fwd."""
     from pose6d._lib import Tuning, call, query, stream
     from pose6d.trunk import DTYPES, pack_single
     N, H, W, Cin, Cout = cfg
@@ -237,7 +239,8 @@ def test_conv3x3_patch(cfg):
     x = torch.randn(N, Cin, H, W, generator=g).bfloat16().float()
     w = (torch.randn(Cout, Cin, 3, 3, generator=g) * (2.0 / (Cin * 9)) ** 0.5).bfloat16().float()
     b = torch.randn(Cout, generator=g) * 0.1
-    assert query("conv_patch_plan", dt, N, H, W, Cin, Cout, 3, 3, 1, 1, H, W) > 0
+    default_patch = query("conv_patch_plan", dt, N, H, W, Cin, Cout, 3, 3, 1, 1, H, W) > 0
+    assert default_patch == (H * W >= 3136)
     xd = _nhwc(x).to("cuda", dtype)
     wp, _ = pack_single(w.cuda(), Cin, dtype, with_t=False)
     bd = b.cuda()
@@ -252,24 +255,32 @@ def test_conv3x3_patch(cfg):
         torch.cuda.synchronize()
         return y.cpu()
 
-    y = fwd()
     ref = F.conv2d(x, w, None, stride=1, padding=1)
-    _close(y.permute(0, 3, 1, 2), ref, 2e-2, "patch fwd")
-    assert torch.equal(fwd(), y), "repeated launch differs"
-    yb = fwd(bias=bd)
+    for st in (2, 3, 4):
+        y = fwd(Tuning(conv_patch=1, conv_stages=st))
+        _close(y.permute(0, 3, 1, 2), ref, 2e-2, f"patch fwd ({st} slots)")
+        assert torch.equal(fwd(Tuning(conv_patch=1, conv_stages=st)), y), "repeated launch differs"
+        if st == 2:
+            y2 = y
+        else:
+            assert torch.equal(y, y2), "the ring depth changed the patch kernel's bits"
+    if default_patch:
+        assert torch.equal(fwd(), y2), "the default plan is not the patch kernel"
+    yb = fwd(Tuning(conv_patch=1), bias=bd)
     _close(yb.permute(0, 3, 1, 2), ref + b.view(1, -1, 1, 1), 2e-2, "patch fwd + bias")
     yg = fwd(Tuning(conv_patch=0))
-    _close(yg, y, 2e-2, "implicit GEMM vs patch")
-    # eval BN-act epilogue == plain store + pose6d_bn_act_fwd, bit for bit
+    _close(yg, y2, 2e-2, "implicit GEMM vs patch")
+    # eval BN-act epilogue == plain store + pose6d_bn_act_fwd, bit for bit (default plans)
     sc = (torch.rand(Cout, generator=g) + 0.5).cuda()
     sh = (torch.randn(Cout, generator=g) * 0.1).cuda()
     fused = torch.empty(N, H, W, Cout, device="cuda", dtype=dtype)
     call("conv2d_fwd_act", dt, xd, wp, bd, fused, N, H, W, Cin, Cout, 3, 3, 1, 1, H, W, sc, sh, None, None, None, 1,
          *skws(), stream())
+    plain = fwd(bias=bd)
     sep = torch.empty(N, H, W, Cout, device="cuda", dtype=dtype)
-    call("bn_act_fwd", dt, yb.cuda(), sc, sh, None, None, None, 1, sep, N * H * W, Cout, stream())
+    call("bn_act_fwd", dt, plain.cuda(), sc, sh, None, None, None, 1, sep, N * H * W, Cout, stream())
     torch.cuda.synchronize()
-    assert torch.equal(fused.cpu(), sep.cpu()), "patch BN-act epilogue != conv + bn_act"
+    assert torch.equal(fused.cpu(), sep.cpu()), "BN-act epilogue != conv + bn_act"
 
 
 SPLITK_CONFIGS = [
