@@ -77,6 +77,15 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
+// one conv's weight-packing record (pose6d_pack_conv_weights, pose6d_adamw_step_packed)
+struct PackDesc {
+  const float* w;   // OIHW fp32 master
+  void* wp;         // [O][Kpad], K = (kh, kw, ci) with ci padded to Ip
+  void* wt;         // [I][KH][KW][O] or null
+  int O, I, Ip, KH, KW, Kpad;
+  int64_t start, count;
+};
+
 inline hipStream_t stream_of(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 __host__ __device__ inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }

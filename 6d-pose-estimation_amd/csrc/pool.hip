@@ -80,13 +80,7 @@ __global__ void nchw4_to_nhwc_kernel(const float* __restrict__ x, T* __restrict_
   }
 }
 
-struct PackDesc {
-  const float* w;   // OIHW fp32
-  void* wp;         // [O][Kpad]
-  void* wt;         // [I][KH][KW][O] or null
-  int O, I, Ip, KH, KW, Kpad;
-  int64_t start, count;
-};
+using p6::PackDesc;
 
 // z = 0: wp[o][k], k = (kh, kw, ci).  1x1 filters (k order == OIHW order): a straight
 //        fp32 -> compute-dtype conversion, 8 elements per thread (two float4 loads, one

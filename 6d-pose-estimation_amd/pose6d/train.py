@@ -11,6 +11,11 @@ MI355X design:
   * the entire step (~400 launches) is captured once into a hipGraph and
     replayed; the AdamW step counter, dropout seed and lr live in device memory
     so replays stay exact;
+  * the AdamW launch also writes the convs' packed compute-dtype weights
+    (pose6d_adamw_step_packed): the next forward reads them with no packing pass
+    over the updated masters.  A write to the masters from outside the step
+    (restore, load_state_dict, ...) is seen through torch's version counters and
+    re-packed before the next step;
   * data parallel: one process per GPU, batch shards, gradient all-reduce over
     RCCL (torch.distributed 'nccl'); bucketed all-reduces are issued on a comm
     stream as soon as each bucket's gradients exist, overlapping the rest of the
@@ -22,9 +27,10 @@ MI355X design:
 """
 import math
 
+import numpy as np
 import torch
 
-from ._lib import call, stream
+from ._lib import Pose6dError, call, query, stream
 from .dist import BucketReducer, plan_buckets
 from .head import HeadEngine
 from .trunk import TrunkEngine
@@ -71,7 +77,7 @@ class RGBDGeometricTrainer:
 
     def __init__(self, model, batch, dtype=torch.bfloat16, lr=1e-4, weight_decay=1e-4, max_norm=1.0,
                  betas=(0.9, 0.999), eps=1e-8, rot_weight=1.0, trans_weight=10.0, process_group=None,
-                 bucket_mb=25.0, tail_mb=2.0, force_buckets=False):
+                 bucket_mb=25.0, tail_mb=2.0, force_buckets=False, pack_in_adamw=True):
         self.model = model
         self.B = batch
         dev = next(model.parameters()).device
@@ -87,6 +93,13 @@ class RGBDGeometricTrainer:
         self.arena = FlatArena(order, dev)
         self.m = torch.zeros_like(self.arena.flat)
         self.v = torch.zeros_like(self.arena.flat)
+        # pack_in_adamw=False: the previous layout (a packing launch at the start of every
+        # step, plain adamw_step) -- kept for A/B timing and the bit-identity test
+        self.pack_in_adamw = pack_in_adamw
+        self._packed_key = None
+        self.sync_weights()
+        if pack_in_adamw:
+            self._build_jobs()
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
         # the bucketed all-reduce path (segmented graphs, comm stream, async collectives):
         # every world > 1, and world 1 with force_buckets (exercises the RCCL branch on a
@@ -118,6 +131,36 @@ class RGBDGeometricTrainer:
         self.pg = process_group
         self.graphs = None
         self._buckets(bucket_mb, tail_mb)
+
+    # ------------------------------------------------------------- packed weights
+    def _build_jobs(self):
+        """The work table of pose6d_adamw_step_packed (plain ranges and 64 x 64 conv
+        tiles over the arena), built once: the arena and the packed buffers never move."""
+        rec = self.trunk._desc_host
+        args = (rec.ctypes.data, len(rec), self.arena.flat.data_ptr(), self.arena.numel)
+        n = query("adamw_packed_jobs", *args, None, 0)
+        if n <= 0:
+            raise Pose6dError(f"pose6d_adamw_packed_jobs failed ({n})")
+        jobs = np.zeros((n, 4), dtype=np.int32)
+        if query("adamw_packed_jobs", *args, jobs.ctypes.data, n) != n:
+            raise Pose6dError("pose6d_adamw_packed_jobs: inconsistent job count")
+        self._jobs = torch.from_numpy(jobs).to(self.dev)
+        self.n_jobs = n
+
+    def _weights_key(self):
+        # writes through the arena (restore) bump flat's counter; writes through a
+        # Parameter (load_state_dict, p.data.copy_) bump that Parameter's own
+        return (self.arena.flat._version,) + tuple(op.conv.weight._version for op in self.trunk.convs)
+
+    def sync_weights(self):
+        """Re-pack the conv weights from the fp32 masters (one launch).  step() calls
+        it when the masters were written from outside the step."""
+        self.trunk.pack_weights(force=True)
+        self._packed_key = self._weights_key()
+
+    def _sync_if_stale(self):
+        if self.pack_in_adamw and self._weights_key() != self._packed_key:
+            self.sync_weights()
 
     # ------------------------------------------------------------- DDP buckets
     def _buckets(self, bucket_mb, tail_mb=0.0):
@@ -158,14 +201,23 @@ class RGBDGeometricTrainer:
         # (the seed is next read by the following step's forward)
         call("sumsq_partial_step", self.arena.grad, self.arena.numel, self.partials, NPART,
              self.hp[5:6], self.seed, st)
-        call("adamw_step", self.arena.flat, self.arena.grad, self.m, self.v, self.arena.numel, self.partials, NPART,
-             self.hp, self.norm, st)
+        if self.pack_in_adamw:   # + the packed conv weights the next step's forward reads
+            call("adamw_step_packed", self.arena.flat, self.arena.grad, self.m, self.v, self.partials, NPART, self.hp,
+                 self.norm, self.trunk.dt, self.trunk._desc_dev, self._jobs, self.n_jobs, st)
+        else:
+            call("adamw_step", self.arena.flat, self.arena.grad, self.m, self.v, self.arena.numel, self.partials,
+                 NPART, self.hp, self.norm, st)
+
+    def _pack(self):
+        if not self.pack_in_adamw:
+            self.trunk.pack_weights(force=True)
 
     def step_eager(self, data):
         """One training step without graphs (reference order of operations)."""
+        self._sync_if_stale()
         if not self._ddp:
             return self.step_body(data)
-        self.trunk.pack_weights(force=True)
+        self._pack()
         self._forward_loss(*data)
         dfeat = self._head_backward()
         self._backward_ddp(dfeat)
@@ -174,7 +226,7 @@ class RGBDGeometricTrainer:
     def step_body(self, data):
         """The one-GPU step's launches, in order (what capture() records for world == 1;
         pose6d.steptime captures it for in-step kernel timing)."""
-        self.trunk.pack_weights(force=True)
+        self._pack()
         self._forward_loss(*data)
         dfeat = self._head_backward()
         self.trunk.backward(dfeat, self.arena.grad_of)
@@ -206,6 +258,7 @@ class RGBDGeometricTrainer:
         """Capture the step.  world == 1: one graph.  world > 1: the forward +
         backward as graph segments cut where a gradient bucket completes, and the
         optimizer as a graph of its own (the all-reduces run between replays)."""
+        self._sync_if_stale()
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -254,7 +307,7 @@ class RGBDGeometricTrainer:
 
         with torch.cuda.stream(cs):
             begin()
-            self.trunk.pack_weights(force=True)
+            self._pack()
             self._forward_loss(*data)
             dfeat = self._head_backward()
             self.trunk.backward(dfeat, self.arena.grad_of, on_conv_done=on_conv)
@@ -269,6 +322,7 @@ class RGBDGeometricTrainer:
         return segs + [(opt, None)]
 
     def step(self, data=None):
+        self._sync_if_stale()
         if self.graphs is None:
             return self.step_eager(data)
         if not self._ddp:

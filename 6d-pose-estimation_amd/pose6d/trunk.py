@@ -339,6 +339,7 @@ class TrunkEngine:
                       op.cin_pad, op.k, op.k, op.Kpad, start, op.cout * op.Kpad)
             start += op.cout * op.Kpad
         self._pack_total = start
+        self._desc_host = rec   # (host copy: pose6d_adamw_packed_jobs reads it)
         self._desc_dev = torch.from_numpy(rec.view(np.uint8).copy()).to(self.device)
         self._desc_ptrs = tuple(op.conv.weight.data_ptr() for op in self.convs)
 

@@ -593,6 +593,21 @@ int pose6d_sumsq_partial_step(const float *g, int64_t n, float *partials, int32_
                               int64_t *seed, void *stream);
 int pose6d_adamw_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
                       const float *partials, int32_t nparts, const float *hp, float *norm_out, void *stream);
+/* The same update (bit-identical), that also writes every conv's packed compute-dtype
+ * copies (wp / wt of pose6d_pack_conv_weights) from the updated values: the next
+ * forward reads them without a packing launch.  Each conv's OIHW master must be a
+ * 16-B aligned slice of param; wp's padding entries are never written (pack once,
+ * with pose6d_pack_conv_weights, before the first step and after any write to the
+ * masters from outside this call).  descs: device copy of the pack table (n_desc
+ * records, see pose6d_pack_conv_weights).  jobs: device copy of the int32 [n_jobs][4]
+ * work table pose6d_adamw_packed_jobs builds on the host from a HOST copy of the same
+ * table (device addresses compared as integers) -- it returns the job count (cap /
+ * jobs may be 0 / NULL to size the table), or a negative error code. */
+int pose6d_adamw_packed_jobs(const void *descs, int32_t n_desc, const float *param, int64_t n, int32_t *jobs,
+                             int32_t cap);
+int pose6d_adamw_step_packed(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
+                             const float *partials, int32_t nparts, const float *hp, float *norm_out, int32_t dtype,
+                             const void *descs, const int32_t *jobs, int32_t n_jobs, void *stream);
 
 #ifdef __cplusplus
 }

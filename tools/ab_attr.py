@@ -4,6 +4,7 @@ median ms per step of each.
 
     python tools/ab_attr.py pose6d.trunk.TrunkEngine.bwd_dual_bn [--rounds 7 --steps 20]
     python tools/ab_attr.py none      # one trainer, as configured (runtime env A/B across processes)
+    python tools/ab_attr.py kw:pack_in_adamw [--dtype f32]   # a trainer keyword False / True
 """
 import argparse
 import importlib
@@ -25,9 +26,13 @@ def main():
     ap.add_argument("attr", help="module.Class.attribute")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     a = ap.parse_args()
-    klass = None
-    if a.attr != "none":
+    dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    klass, kw = None, None
+    if a.attr.startswith("kw:"):
+        kw = a.attr[3:]
+    elif a.attr != "none":
         mod, cls, attr = a.attr.rsplit(".", 2)
         klass = getattr(importlib.import_module(mod), cls)
     from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
@@ -35,11 +40,12 @@ def main():
     dev = torch.device("cuda", 0)
     data = synth_batch(32, dev, seed=1000)
     trs = {}
-    for val in ((False, True) if klass else (True,)):
+    for val in ((False, True) if (klass or kw) else (True,)):
         if klass:
             setattr(klass, attr, val)
         torch.manual_seed(0)
-        tr = RGBDGeometricTrainer(PoseNetRGBDGeometric(pretrained=False).to(dev), 32, dtype=torch.bfloat16)
+        tr = RGBDGeometricTrainer(PoseNetRGBDGeometric(pretrained=False).to(dev), 32, dtype=dtype,
+                                  **({kw: val} if kw else {}))
         tr.capture(data)
         for _ in range(3):
             tr.step(data)
