@@ -16,6 +16,7 @@
 
 #include <type_traits>
 
+#include "bn_fold.h"
 #include "common.h"
 
 namespace {
@@ -139,8 +140,15 @@ __global__ __launch_bounds__(kThreads) void bn_stats_finalize_kernel(
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
     float momentum, float eps, float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ smean,
     float* __restrict__ sinv) {
-  bn_stats_finalize_body<L>(blockIdx.x, part, rows, C, M, gamma, beta, rmean, rvar, nbt, momentum, eps, scale, shift,
-                            smean, sinv);
+  if constexpr (L == 64) {
+    // <= 512 rows: one channel per wave, the arithmetic the producing convolution's
+    // in-launch finalize shares (bn_fold.h)
+    const pose6d_bn_stats_t d{part, gamma, beta, rmean, rvar, nbt, scale, shift, smean, sinv, momentum, eps, C};
+    p6::bn_fold_wave<1>(d, [&](int64_t i) { return part[i]; }, rows, M, blockIdx.x * 4 + (threadIdx.x >> 6), 1);
+  } else {
+    bn_stats_finalize_body<L>(blockIdx.x, part, rows, C, M, gamma, beta, rmean, rvar, nbt, momentum, eps, scale,
+                              shift, smean, sinv);
+  }
 }
 
 // two BatchNorms over the same output grid (a downsampling block's bn3 and its
@@ -151,6 +159,11 @@ __global__ __launch_bounds__(kThreads) void bn_stats_finalize2_kernel(pose6d_bn_
                                                                       int rows, int64_t M) {
   const pose6d_bn_stats_t& d = blockIdx.y ? b : a;
   if ((int)blockIdx.x * (kThreads / L) >= d.C) return;
+  if constexpr (L == 64) {
+    const float* part = d.partial;
+    p6::bn_fold_wave<1>(d, [&](int64_t i) { return part[i]; }, rows, M, blockIdx.x * 4 + (threadIdx.x >> 6), 1);
+    return;
+  }
   bn_stats_finalize_body<L>(blockIdx.x, d.partial, rows, d.C, M, d.gamma, d.beta, d.running_mean, d.running_var,
                             d.num_batches, d.momentum, d.eps, d.scale, d.shift, d.save_mean, d.save_invstd);
 }
