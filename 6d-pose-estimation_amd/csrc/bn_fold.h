@@ -1,8 +1,10 @@
 // The BatchNorm2d training finalize of one channel on one wave: the arithmetic of
-// pose6d_bn_finalize for statistics with <= 512 partial rows, shared by its own
-// kernel (bn.hip) and by the convolutions that finalize their BN in the launch that
-// produced the statistics (conv_igemm.hip, pose6d_conv2d_fwd_bn) -- one code path, so
-// both give the same bits.
+// pose6d_bn_finalize for statistics with <= 512 partial rows (bn.hip's single and dual
+// finalize kernels).  Written so that any kernel can fold channels with the same bits:
+// round 5 ran it inside the producing conv (the column's last workgroup folding its
+// channels) -- bit-identical, but a serial tail of ~30 us per conv against the ~5 us
+// launch it saved (profiles/r05f_bn_fold_rejected.txt), so only the finalize kernels
+// use it.
 //
 // Partials are [2][C][rows] fp32 (row i: sum and M2 about the block mean of 32
 // output pixels; the last row may hold fewer).  Lane l folds rows l, l + 64, ... in

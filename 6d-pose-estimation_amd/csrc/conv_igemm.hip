@@ -20,7 +20,6 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "bn_fold.h"
 #include "common.h"
 #include "lds_dma.h"
 #include "wgrad_body.h"
@@ -80,13 +79,6 @@ struct Geom {
   int splits;
   int* sk_cnt;
   float* sk_part;
-  // BatchNorm finalize in the launch (pose6d_conv2d_fwd_bn; forward kGemm / kFwd with
-  // statistics): null bnf_cnt = off.  The epilogue writes the statistics partials
-  // write-through (sc1); after its stores each workgroup adds 1 to its output-channel
-  // column's counter bnf_cnt[tn] (agent scope), and the column's last arriver re-arms
-  // the counter and folds the column's channels (bn_fold.h, sc1 loads) into bnf.
-  pose6d_bn_stats_t bnf;
-  int* bnf_cnt;
 };
 
 // ---------------------------------------------------------------------------
@@ -109,40 +101,6 @@ struct Geom {
 // counter block has a fixed size so that every plan run on one workspace finds its
 // counters at the same words; the caller zeroes it once (every launch leaves it
 // zero).  Size query: pose6d_conv_splitk_workspace.
-// statistics rows a workgroup folds in the launch (four per lane: the fold's registers
-// stay under the conv's own budget; layer3 / layer4 at batch 32 have 196 / 49)
-constexpr int kBnFoldMaxRows = 256;
-
-// The column's last workgroup folds its BatchNorm channels [n0, n0 + BN) (see Geom::bnf).
-// Compiled into the BNF kernel instances only (its loads in flight would otherwise set
-// the register budget of every forward kernel)
-template <int BN, int NW>
-__device__ __forceinline__ void bn_fold_arrive(const Geom& g, char* smem, const float* stats, int tn, int n0) {
-  constexpr int SC1 = 16;   // buffer cache-policy bits: sc1
-  const int tid = threadIdx.x;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's statistics stores acknowledged
-  __syncthreads();                                   // ... every wave's; LDS free for the flag
-  int* flag = reinterpret_cast<int*>(smem);
-  if (tid == 0) flag[0] = __hip_atomic_fetch_add(&g.bnf_cnt[tn], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  const bool last = flag[0] == g.gm - 1;
-  if (!last) return;
-  if (tid == 0) __hip_atomic_store(&g.bnf_cnt[tn], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int rows = (g.M + 31) >> 5;
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(stats), 0, 2 * g.Ncols * rows * 4, 0x00020000);
-  auto ld = [&](int64_t i) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)i * 4, 0, SC1));
-  };
-  const int wave = tid >> 6;
-  constexpr int PER = BN / NW;   // channels per wave
-  const int c0 = n0 + wave * PER;
-  const int nch = c0 < g.Ncols ? (g.Ncols - c0 < PER ? g.Ncols - c0 : PER) : 0;
-  // channels in flight per wave x partial rows per lane, by the row count (registers)
-  if (rows <= 64) p6::bn_fold_wave<8, 1>(g.bnf, ld, rows, g.M, c0, nch);
-  else p6::bn_fold_wave<4, 4>(g.bnf, ld, rows, g.M, c0, nch);
-}
-
 constexpr int kSkMaxTiles = 8192;                       // plans with more tiles never split
 constexpr int64_t kSkCntBytes = (int64_t)kSkMaxTiles * 4;   // 32 KiB
 
@@ -485,17 +443,8 @@ __device__ __forceinline__ void conv_epilogue(f32x4 (&acc)[BM / (16 * (NW / 2))]
         if (lane < 16 && c < g.Ncols && nval > 0) {
           // channel-major [2][C][rows]: the finalize reads each channel's rows coalesced
           const int64_t rows = (g.M + 31) >> 5;
-          if (g.bnf_cnt) {   // folded in this launch: write-through for the folding workgroup
-            const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(stats, 0, (int)(2 * g.Ncols * rows * 4), 0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s), rs,
-                                                  (int)((int64_t)c * rows + (rb >> 5)) * 4, 0, 16);
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, q), rs,
-                                                  (int)(((int64_t)g.Ncols + c) * rows + (rb >> 5)) * 4, 0, 16);
-          } else {
-            stats[(int64_t)c * rows + (rb >> 5)] = s;
-            stats[((int64_t)g.Ncols + c) * rows + (rb >> 5)] = q;
-          }
+          stats[(int64_t)c * rows + (rb >> 5)] = s;
+          stats[((int64_t)g.Ncols + c) * rows + (rb >> 5)] = q;
         }
       }
     }
@@ -870,7 +819,7 @@ template <typename T> struct LK { static constexpr int CH = 16 / (int)sizeof(T),
 #define POSE6D_EPI_PRE 1
 #endif
 template <typename T, int BM, int BN, int MODE, int S, bool ACT = false, int NW = 4, bool BNR = false,
-          bool PRE = false, bool BNF = false>
+          bool PRE = false>
 __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* __restrict__ src,
                                               const T* __restrict__ wts, const float* __restrict__ bias,
                                               const T* __restrict__ res, T* __restrict__ out,
@@ -1263,20 +1212,16 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   else
     conv_epilogue<T, BM, BN, ACT ? 1 : 0, NW, false, BNR>(acc, smem, g, bias, res, out, stats, m0, n0, cls, nullptr,
                                                           pre, early);
-  if constexpr (BNF) {
-    if (g.bnf_cnt && stats) bn_fold_arrive<BN, NW>(g, smem, stats, tn, n0);
-  }
 }
 
 // BNR: data gradient with the BatchNorm-reduce epilogue (its own instance: the
 // forward 1x1 kernels, kGemm too, keep their register budget)
-// BNF: forward with the BatchNorm finalize in the launch (Geom::bnf; its own instance)
-template <typename T, int BM, int BN, int MODE, int S, bool ACT, int NW, bool BNR = false, bool BNF = false>
+template <typename T, int BM, int BN, int MODE, int S, bool ACT, int NW, bool BNR = false>
 __global__ __launch_bounds__(64 * NW) void conv_lds_kernel(const T* __restrict__ src, const T* __restrict__ wts,
                                                            const float* __restrict__ bias, const T* __restrict__ res,
                                                            T* __restrict__ out, float* __restrict__ stats, Geom g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv_lds_body<T, BM, BN, MODE, S, ACT, NW, BNR, false, BNF>(smem, blockIdx.x, src, wts, bias, res, out, stats, g);
+  conv_lds_body<T, BM, BN, MODE, S, ACT, NW, BNR>(smem, blockIdx.x, src, wts, bias, res, out, stats, g);
 }
 
 #include "conv_patch.h"
@@ -1360,14 +1305,6 @@ int launch_fast(const Geom& g0, const void* src, const void* w, const float* bia
   if constexpr (MODE == kGemm || MODE == kFwd || MODE == kGemmDual) {
     if (g.act) {   // eval BN-act epilogue (pose6d_conv2d_fwd_act)
       conv_lds_kernel<T, BM, BN, MODE, S, true, NW><<<grid, 64 * NW, lds, s>>>(
-          (const T*)src, (const T*)w, bias, (const T*)res, (T*)out, stats, g);
-      P6_LAUNCH_CHECK();
-      return POSE6D_OK;
-    }
-  }
-  if constexpr (MODE == kGemm || MODE == kFwd) {
-    if (g.bnf_cnt) {   // forward + the BatchNorm finalize (pose6d_conv2d_fwd_bn)
-      conv_lds_kernel<T, BM, BN, MODE, S, false, NW, false, true><<<grid, 64 * NW, lds, s>>>(
           (const T*)src, (const T*)w, bias, (const T*)res, (T*)out, stats, g);
       P6_LAUNCH_CHECK();
       return POSE6D_OK;
@@ -1699,27 +1636,10 @@ int64_t splitk_need(const Plan& p) {
   return kSkCntBytes + tiles * p.g.splits * bm * bn * 4;
 }
 
-// in-launch BatchNorm finalize (pose6d_conv2d_fwd_bn): the forward LDS-DMA plans with
-// statistics of <= kBnFoldMaxRows rows
-bool bn_fold_ok(const Plan& p, const float* stats) {
-  return p.fast && stats && (p.mode == kGemm || p.mode == kFwd) && ((p.g.M + 31) >> 5) <= kBnFoldMaxRows;
-}
-
 int run_conv(int dtype, int mode, const Geom& g, const void* src, const void* w, const float* bias, const void* res,
              void* out, float* stats, hipStream_t s, const pose6d_tuning_t* tn = nullptr, bool fwd = false,
-             void* sk_ws = nullptr, int64_t sk_bytes = 0, const pose6d_bn_stats_t* bnf = nullptr,
-             int* bnf_cnt = nullptr) {
+             void* sk_ws = nullptr, int64_t sk_bytes = 0) {
   Plan p = choose(dtype, mode, g, false, tn, fwd);
-  if (bnf && bnf_cnt && bn_fold_ok(p, stats)) {
-    p.g.bnf = *bnf;
-    p.g.bnf_cnt = bnf_cnt;
-  } else if (bnf) {   // not foldable in this plan: the finalize launch follows the conv
-    const int rc = run_conv(dtype, mode, g, src, w, bias, res, out, stats, s, tn, fwd, sk_ws, sk_bytes);
-    if (rc != POSE6D_OK) return rc;
-    return pose6d_bn_finalize(stats, (g.M + 31) >> 5, bnf->C, g.M, bnf->gamma, bnf->beta, bnf->running_mean,
-                              bnf->running_var, bnf->num_batches, bnf->momentum, bnf->eps, 1, bnf->scale, bnf->shift,
-                              bnf->save_mean, bnf->save_invstd, nullptr, s);
-  }
   const int64_t need = splitk_need(p);
   if (need > 0) {
     P6_CHECK_ARG(sk_ws != nullptr && sk_bytes >= need,
@@ -1805,39 +1725,6 @@ extern "C" int pose6d_conv2d_fwd_tuned(int32_t dtype, const void* x, const void*
   if (mode == kGemm) P6_CHECK_ARG(Cin % bk == 0, "pose6d_conv2d_fwd: 1x1 Cin %% %d != 0", bk);
   return run_conv(dtype, mode, g, x, w, bias, nullptr, y, stats, p6::stream_of(stream), tuning, true, splitk_ws,
                   splitk_ws_bytes);
-}
-
-extern "C" int pose6d_conv2d_fwd_bn(int32_t dtype, const void* x, const void* w, const float* bias, void* y,
-                                    float* stats, const pose6d_bn_stats_t* bn, int32_t* col_cnt, int32_t N, int32_t H,
-                                    int32_t W, int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
-                                    int32_t pad, int32_t Ho, int32_t Wo, const pose6d_tuning_t* tuning,
-                                    void* splitk_ws, int64_t splitk_ws_bytes, void* stream) {
-  P6_CHECK_ARG(dtype == POSE6D_DT_F32 || dtype == POSE6D_DT_BF16, "pose6d_conv2d_fwd_bn: bad dtype %d", dtype);
-  P6_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cout > 0 && Cout % 8 == 0, "pose6d_conv2d_fwd_bn: bad shape (Cout %% 8)");
-  P6_CHECK_ARG(Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1,
-               "pose6d_conv2d_fwd_bn: Ho/Wo inconsistent");
-  P6_CHECK_ARG(stats && bn && bn->C == Cout && bn->partial == stats,
-               "pose6d_conv2d_fwd_bn: needs statistics and a BatchNorm over its Cout channels reading them");
-  P6_CHECK_ARG(col_cnt == nullptr || ((uintptr_t)col_cnt & 3) == 0, "pose6d_conv2d_fwd_bn: bad counter block");
-  const int bk = dtype == POSE6D_DT_BF16 ? 32 : 16;
-  int mode;
-  const Geom g = fwd_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
-  if (mode == kFwd)
-    P6_CHECK_ARG(g.log2SC >= 0 && Cin % bk == 0,
-                 "pose6d_conv2d_fwd_bn: Cin must be 4 or a power of two >= %d (got %d)", bk, Cin);
-  if (mode == kGemm) P6_CHECK_ARG(Cin % bk == 0, "pose6d_conv2d_fwd_bn: 1x1 Cin %% %d != 0", bk);
-  return run_conv(dtype, mode, g, x, w, bias, nullptr, y, stats, p6::stream_of(stream), tuning, true, splitk_ws,
-                  splitk_ws_bytes, bn, col_cnt);
-}
-
-// 1 when pose6d_conv2d_fwd_bn of this geometry finalizes the BatchNorm inside the conv launch
-extern "C" int pose6d_conv_bn_fold(int32_t dtype, const pose6d_tuning_t* tuning, int32_t N, int32_t H, int32_t W,
-                                   int32_t Cin, int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad,
-                                   int32_t Ho, int32_t Wo) {
-  int mode;
-  const Geom g = fwd_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
-  static float dummy;
-  return bn_fold_ok(choose(dtype, mode, g, false, tuning, true), &dummy) ? 1 : 0;
 }
 
 // eval-mode conv + BatchNorm apply (+ residual, + ReLU) in one launch: the store of

@@ -265,13 +265,6 @@ class TrunkEngine:
         # launch; partial tiles): engines on different streams never share one
         self.ws_sk = torch.zeros(max(ws_sk, 1), device=device, dtype=torch.uint8) if ws_sk else None
         self.ws_sk_bytes = ws_sk
-        # training forward: convs whose BN finalize runs inside the conv launch
-        # (pose6d_conv2d_fwd_bn; its per-column arrival counters, left zero by every launch)
-        self.bnf_cnt = torch.zeros(64, device=device, dtype=torch.int32)
-        self.bnf_ops = {op for op in self.convs
-                        if op.bn is not None and max(op.cout // 64, 1) <= 64 and
-                        query("conv_bn_fold", self.dt, None, B, op.H, op.W, op.cin_pad, op.cout, op.k, op.k,
-                              op.stride, op.pad, op.Ho, op.Wo) == 1}
         self.feat = f32(B, self.feat_dim)
         self.feat_grad_in = None
         self._fold_dev, self._fold_key = None, None
@@ -391,14 +384,13 @@ class TrunkEngine:
         # training: a downsampling block's two BN finalizes (bn3, downsample BN: same
         # output grid) as one launch after conv3 (pose6d_bn_finalize_dual)
         fin2 = {}
-        bnf = self.bnf_ops if (training and not fold and self.bn_fold_fwd) else ()
         if training and not fold and self.bn_dual_finalize:
             pos = {id(o): i for i, o in enumerate(self.ops)}
             for op in self.ops:
                 if isinstance(op, _ActOp) and op.res_conv is not None:
                     c3, r = op.cop, op.res_conv
                     if (pos[id(r)] < pos[id(c3)] and c3.stats_rows == r.stats_rows
-                            and (c3.Ho, c3.Wo) == (r.Ho, r.Wo) and c3 not in bnf and r not in bnf):
+                            and (c3.Ho, c3.Wo) == (r.Ho, r.Wo)):
                         fin2[c3] = r
                         fin2[r] = None
         for op in self.ops:
@@ -429,12 +421,6 @@ class TrunkEngine:
                     call("conv2d_fwd_act", dt, op.src.t, op.wp, bias, a.out.t, B, op.H, op.W, op.cin_pad, op.cout,
                          op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, op.scale, op.shift, res, rs, rb, int(a.relu),
                          self.ws_sk, self.ws_sk_bytes, st)
-                    continue
-                if op in bnf:   # conv + its BN's finalize, one launch
-                    d = _bn_stats(op)
-                    call("conv2d_fwd_bn", dt, op.src.t, op.wp, bias, op.out.t, op.stats, ctypes.addressof(d),
-                         self.bnf_cnt, B, op.H, op.W, op.cin_pad, op.cout, op.k, op.k, op.stride, op.pad, op.Ho,
-                         op.Wo, None, self.ws_sk, self.ws_sk_bytes, st)
                     continue
                 call("conv2d_fwd", dt, op.src.t, op.wp, bias, op.out.t, op.stats if training else None, B, op.H,
                      op.W, op.cin_pad, op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, self.ws_sk,
@@ -669,9 +655,6 @@ class TrunkEngine:
     # training forward: a downsampling block's two BN finalizes in one launch
     # (bit-identical to two pose6d_bn_finalize calls; attribute for the tests)
     bn_dual_finalize = True
-    # training forward: the BN finalize inside the producing conv's launch where the plan
-    # allows it (pose6d_conv2d_fwd_bn, bit-identical; attribute for the tests / A/B)
-    bn_fold_fwd = True
     # training backward: a BN + ReLU whose output gradient one data-gradient launch
     # completes gets its reduce pass from that launch's epilogue (attribute for the tests)
     bwd_conv_bn_reduce = True

@@ -420,21 +420,6 @@ typedef struct {
 } pose6d_bn_stats_t;
 int pose6d_bn_finalize_dual(const pose6d_bn_stats_t *a, const pose6d_bn_stats_t *b, int32_t rows, int64_t count,
                             void *stream);
-/* pose6d_conv2d_fwd (with statistics) followed by pose6d_bn_finalize (training) of
- * the BatchNorm `bn` (bn->partial == stats, bn->C == Cout), bit for bit, in ONE launch
- * where the plan allows it (pose6d_conv_bn_fold: the LDS-DMA forward plans whose
- * statistics have <= 256 rows, i.e. layer3 / layer4 at batch 32): the last workgroup
- * to finish each output-channel column folds that column's statistics.  Otherwise
- * the finalize launch follows the conv.  col_cnt: caller-provided arrival counters,
- * >= ceil(Cout / 64) int32, zeroed once (every launch leaves them zero; one block per
- * stream -- launches sharing a block must be stream-ordered); NULL = two launches.
- * tuning: as pose6d_conv2d_fwd_tuned (may be NULL). */
-int pose6d_conv2d_fwd_bn(int32_t dtype, const void *x, const void *w, const float *bias, void *y, float *stats,
-                         const pose6d_bn_stats_t *bn, int32_t *col_cnt, int32_t N, int32_t H, int32_t W, int32_t Cin,
-                         int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
-                         const pose6d_tuning_t *tuning, void *splitk_ws, int64_t splitk_ws_bytes, void *stream);
-int pose6d_conv_bn_fold(int32_t dtype, const pose6d_tuning_t *tuning, int32_t N, int32_t H, int32_t W, int32_t Cin,
-                        int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo);
 /* Eval-mode fold of a table of BatchNorms in one launch: per entry and channel c,
  * scale = gamma / sqrt(running_var + eps), shift = beta - running_mean * scale,
  * save_mean = running_mean, save_invstd = 1 / sqrt(running_var + eps) -- pose6d_bn_finalize

@@ -360,65 +360,6 @@ def test_conv_splitk(cfg, dtype):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("cfg", SPLITK_CONFIGS + [(32, 14, 14, 256, 256, 3, 1, 1), (32, 7, 7, 512, 2048, 1, 1, 0),
-                                                  (32, 14, 14, 1024, 256, 1, 1, 0), (1, 2, 2, 64, 72, 1, 1, 0)])
-def test_conv_fwd_bn_fold(cfg, dtype):
-    """pose6d_conv2d_fwd_bn: the BatchNorm training finalize done by the last workgroup
-    of each output-channel column inside the conv launch equals pose6d_conv2d_fwd +
-    pose6d_bn_finalize bit for bit (y, statistics, scale / shift, saved mean / invstd,
-    running statistics, num_batches_tracked) -- over tiles, ring depths and split-K
-    plans, and on a repeated launch (the column counters re-arm themselves)."""
-    import ctypes
-    from pose6d._lib import Tuning, call, query, stream
-    from pose6d.trunk import DTYPES, _BnStats, pack_single
-    N, H, W, Cin, Cout, k, s, p = cfg
-    g = torch.Generator().manual_seed(5)
-    dev = "cuda"
-    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
-    x = torch.randn(N, Cin, H, W, generator=g)
-    w = torch.randn(Cout, Cin, k, k, generator=g) * (2.0 / (Cin * k * k)) ** 0.5
-    gamma, beta = torch.rand(Cout, generator=g) + 0.5, torch.randn(Cout, generator=g) * 0.1
-    rm0, rv0 = torch.randn(Cout, generator=g) * 0.1, torch.rand(Cout, generator=g) + 0.5
-    dt = DTYPES[dtype]
-    xd = _nhwc(x).to(dev, dtype)
-    wp, _ = pack_single(w.to(dev), Cin, dtype)
-    rows = query("conv_stats_rows", N, Ho, Wo, Cout)
-    cnt = torch.zeros(64, device=dev, dtype=torch.int32)
-
-    def run(fold, **kw):
-        tn = Tuning(**kw)
-        y = torch.empty(N, Ho, Wo, Cout, device=dev, dtype=dtype)
-        st = torch.empty(2, Cout, rows, device=dev)
-        out = [gamma.to(dev), beta.to(dev), rm0.clone().to(dev), rv0.clone().to(dev),
-               torch.zeros(1, device=dev, dtype=torch.int64)] + [torch.empty(Cout, device=dev) for _ in range(4)]
-        d = _BnStats(st.data_ptr(), *[t.data_ptr() for t in out], 0.1, 1e-5, Cout)
-        if fold:
-            call("conv2d_fwd_bn", dt, xd, wp, None, y, st, ctypes.addressof(d), cnt, N, H, W, Cin, Cout, k, k, s, p,
-                 Ho, Wo, tn.ref, *skws(), stream())
-        else:
-            call("conv2d_fwd_tuned", dt, xd, wp, None, y, st, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo, tn.ref,
-                 *skws(), stream())
-            call("bn_finalize", st, rows, Cout, N * Ho * Wo, *out[:5], 0.1, 1e-5, 1, *out[5:], None, stream())
-        torch.cuda.synchronize()
-        return [y.cpu(), st.cpu()] + [t.cpu() for t in out[2:]]
-
-    folded_any = False
-    for kw in ({}, {"conv_splitk": 3}, {"conv_tile": 3, "conv_stages": 2}, {"conv_tile": 4, "conv_stages": 4},
-               {"conv_tile": 5, "conv_splitk": 2}):
-        folded_any |= query("conv_bn_fold", dt, Tuning(**kw).ref, N, H, W, Cin, Cout, k, k, s, p, Ho, Wo) == 1
-        ref = run(False, **kw)
-        for rep in range(2):
-            got = run(True, **kw)
-            names = ("y", "stats", "running_mean", "running_var", "num_batches", "scale", "shift", "mean", "invstd")
-            for a, b, what in zip(ref, got, names):
-                assert torch.equal(a, b), f"{what} differs ({kw}, launch {rep})"
-        assert int(got[4]) == 1
-    assert folded_any == (rows <= 256), "the fold applies to every forward plan with <= 256 statistics rows"
-    assert int(cnt.abs().sum()) == 0, "column counters left armed"
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_conv_splitk_workspace_contract(dtype):
     """The split-K scratch is the caller's (include/pose6d.h, pose6d_conv_splitk_workspace):
     a plan that splits refuses a missing / short workspace, and split-K forwards running
