@@ -80,10 +80,12 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // one conv's weight-packing record (pose6d_pack_conv_weights, pose6d_adamw_step_packed)
 struct PackDesc {
   const float* w;   // OIHW fp32 master
-  void* wp;         // [O][Kpad], K = (kh, kw, ci) with ci padded to Ip
+  void* wp;         // [O][Kpad], K = (kh, kw', ci): ci padded to Ip, KWp taps kw' per kernel row
   void* wt;         // [I][KH][KW][O] or null
   int O, I, Ip, KH, KW, Kpad;
-  int64_t start, count;
+  int KWp;          // packed taps per kernel row (KW; the row-tap stems: 8, filter tap kw at kw + KWp - KW)
+  int reserved;
+  int64_t start;    // (host bookkeeping: running sum of O * Kpad)
 };
 
 inline hipStream_t stream_of(void* s) { return reinterpret_cast<hipStream_t>(s); }

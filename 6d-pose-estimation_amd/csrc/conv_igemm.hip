@@ -39,7 +39,17 @@ template <> struct KT<float> { static constexpr int VEC = 4; static constexpr in
 // launch -- K-steps [0, Kpad) are the block's 1x1 GEMM over src, the rest the 1x1
 // (stride2) downsample over src2 with weights wts2, summed into a second accumulator
 // set; the epilogue applies both BatchNorms exactly as the separate launches did.
-enum Mode { kGemm = 0, kFwd = 1, kFwdNarrow = 2, kDgrad = 3, kDgradS2 = 4, kGemmDual = 5 };
+enum Mode { kGemm = 0, kFwd = 1, kFwdNarrow = 2, kDgrad = 3, kDgradS2 = 4, kGemmDual = 5, kFwdRowTap = 6 };
+
+// Row-tap forward (kFwdRowTap: the 4-channel stems, 7x7 / stride 2 / pad 3): K is
+// ordered (kernel row kh, tap kw' = kw + 1 in 0..7, channel c), the filter packed with
+// kRowTaps taps per kernel row and a zero tap in front (pose6d_conv_pack_geom), so the
+// 8 taps x 4 channels of one kernel row of one output pixel are 8 consecutive input
+// pixels -- 64 contiguous bytes (bf16) starting at an even pixel (2 ox - pad - 1): the
+// LDS-DMA A tile fetches them as four aligned 16-B chunks (fp32: two kernel rows' worth
+// per 128-B K-step row becomes one row, 32 elements).  Replaces the register-staged
+// 8-byte gather of kFwdNarrow for these convs.
+constexpr int kRowTaps = 8;
 
 struct Geom {
   int M, Ncols, K, Kpad;   // GEMM dims; Kpad = weight row length
@@ -911,6 +921,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
       a_pix[i] = n * g.SH * g.SW;
       if (MODE == kDgrad) { a_y[i] = y + g.pad; a_x[i] = x + g.pad; }
       else if (MODE == kDgradS2) { a_y[i] = y; a_x[i] = x; }
+      else if (MODE == kFwdRowTap) { a_y[i] = y * g.stride - g.pad; a_x[i] = x * g.stride - g.pad - (kRowTaps - g.KW); }
       else { a_y[i] = y * g.stride - g.pad; a_x[i] = x * g.stride - g.pad; }
     }
   }
@@ -944,7 +955,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   // there (uniform branch) and each K-step only adds the channel offset c0 --
   // the per-step address arithmetic that made these kernels issue-bound at one
   // workgroup per CU.  issue() is called with consecutive kt.
-  int tap_len = (MODE == kGemm || DUAL) ? g.Kpad : g.SC;
+  int tap_len = (MODE == kGemm || DUAL) ? g.Kpad : (MODE == kFwdRowTap ? KS : g.SC);   // row-tap: one K-step
   int c0 = 0, kh = kh0, kw = kw0, tw = 0, tap_koff = MODE == kDgradS2 ? (kh0 * g.KW + kw0) * g.SC : 0;
   const T* a_base[A_INS];
   unsigned a_mask[A_INS];
@@ -963,6 +974,15 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
             continue;
           }
         }
+      } else if (MODE == kFwdRowTap) {
+        // K-step kh: this lane's 16-B chunk (logical chunk a_ck / CH) is kernel row kr,
+        // taps 4 x2 .. (8 elements = 2 pixels bf16, 4 = 1 pixel fp32) of that row
+        const int ke = kh * KS + a_ck[i];
+        const int kr = ke >> 5, sy = a_y[i] + kr, sx = a_x[i] + ((ke & 31) >> 2);
+        ok = ok && kr < g.KH && (unsigned)sy < (unsigned)g.SH && (unsigned)sx < (unsigned)g.SW;
+        a_base[i] = ok ? src + ((int64_t)(a_pix[i] + sy * g.SW + sx) << 2) : reinterpret_cast<const T*>(zp);
+        a_mask[i] = ok ? ~0u : 0u;
+        continue;
       } else {
         int sy, sx;
         if (MODE == kFwd) {
@@ -1018,6 +1038,9 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
         kw += 2;
         if (++tw == ntx) { tw = 0; kw = kw0; kh += 2; }
         tap_koff = (kh * g.KW + kw) * g.SC;
+      } else if (MODE == kFwdRowTap) {   // kh counts K-steps
+        ++kh;
+        tap_koff += KS;
       } else {
         if (++kw == g.KW) { kw = 0; ++kh; }
         tap_koff += g.SC;
@@ -1356,6 +1379,15 @@ int dispatch_fast_t(int mode, const Geom& g, int tile, int stages, const void* s
   switch (mode) {
     case kGemm: return launch_fast_mode<T, kGemm>(g, tile, stages, src, w, bias, res, out, stats, s);
     case kFwd: return launch_fast_mode<T, kFwd>(g, tile, stages, src, w, bias, res, out, stats, s);
+    case kFwdRowTap:   // (few instances: 64x64 or 128x64 tiles, 2 / 3 / 4 slots)
+      if (tile == 1 || tile == 5) {
+        if (stages >= 4) return launch_fast<T, 128, 64, kFwdRowTap, 4, 4>(g, src, w, bias, res, out, stats, s);
+        if (stages == 3) return launch_fast<T, 128, 64, kFwdRowTap, 3, 4>(g, src, w, bias, res, out, stats, s);
+        return launch_fast<T, 128, 64, kFwdRowTap, 2, 4>(g, src, w, bias, res, out, stats, s);
+      }
+      if (stages >= 4) return launch_fast<T, 64, 64, kFwdRowTap, 4, 4>(g, src, w, bias, res, out, stats, s);
+      if (stages == 3) return launch_fast<T, 64, 64, kFwdRowTap, 3, 4>(g, src, w, bias, res, out, stats, s);
+      return launch_fast<T, 64, 64, kFwdRowTap, 2, 4>(g, src, w, bias, res, out, stats, s);
     case kDgradS2: return launch_fast_mode<T, kDgradS2>(g, tile, stages, src, w, bias, res, out, stats, s);
     case kGemmDual: return launch_fast_s<T, 64, 64, kGemmDual>(g, stages, src, w, bias, res, out, stats, s);
     default: return launch_fast_mode<T, kDgrad>(g, tile, stages, src, w, bias, res, out, stats, s);
@@ -1445,6 +1477,7 @@ extern "C" int pose6d_conv_stats_rows(int32_t N, int32_t Ho, int32_t Wo, int32_t
 // product entry points never take one, so each conv has one plan (one summation order).
 bool fast_ok(int dtype, int mode, const Geom& g) {
   if (mode == kFwdNarrow) return false;
+  if (mode == kFwdRowTap) return true;   // its only path (fwd_geom checked the geometry)
   if (mode == kGemmDual) {
     const int ks2 = dtype == POSE6D_DT_BF16 ? 64 : 32;
     return g.K % ks2 == 0 && g.Kpad == g.K && g.Kpad2 % ks2 == 0;
@@ -1673,15 +1706,29 @@ int run_conv(int dtype, int mode, const Geom& g, const void* src, const void* w,
                                  : dispatch<float>(mode, g, p.tile, src, w, bias, res, out, stats, s);
 }
 
+// Packed filter layout of a forward conv (the wp operand): taps per kernel row (KW, or
+// kRowTaps for the row-tap stems) and the padded K, a multiple of the K-step of every
+// kernel that reads it.  pose6d_conv_pack_geom exports it.
+int pack_geom(int dtype, int Cin, int KH, int KW, int stride, int pad, int* kwp) {
+  // the first tap pixel 2 ox - pad - (kRowTaps - KW) is even (16-B aligned chunks)
+  const bool rowtap = Cin == 4 && stride == 2 && KH > 1 && KW <= kRowTaps && ((pad + kRowTaps - KW) & 1) == 0;
+  *kwp = rowtap ? kRowTaps : KW;
+  const int ks = dtype == POSE6D_DT_BF16 ? 64 : 32;   // LDS-DMA K-step
+  const int bk = rowtap ? ks : (dtype == POSE6D_DT_BF16 ? 32 : 16);
+  return p6::ceil_div(KH * *kwp * Cin, bk) * bk;
+}
+
 Geom fwd_geom(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad, int Ho, int Wo,
               int* mode) {
-  const int bk = dtype == POSE6D_DT_BF16 ? 32 : 16;
   Geom g{};
-  g.M = N * Ho * Wo; g.Ncols = Cout; g.K = KH * KW * Cin;
-  g.Kpad = p6::ceil_div(g.K, bk) * bk;
+  int kwp = 0;
+  g.M = N * Ho * Wo; g.Ncols = Cout;
+  g.Kpad = pack_geom(dtype, Cin, KH, KW, stride, pad, &kwp);
+  g.K = kwp == kRowTaps ? g.Kpad : KH * KW * Cin;
   g.SH = H; g.SW = W; g.SC = Cin; g.log2SC = ilog2(Cin); g.RH = Ho; g.RW = Wo;
   g.KH = KH; g.KW = KW; g.stride = stride; g.pad = pad;
   if (KH == 1 && KW == 1 && stride == 1 && pad == 0) *mode = kGemm;
+  else if (kwp == kRowTaps) *mode = kFwdRowTap;
   else if (Cin == 4) *mode = kFwdNarrow;
   else *mode = kFwd;
   return g;
@@ -1723,8 +1770,17 @@ extern "C" int pose6d_conv2d_fwd_tuned(int32_t dtype, const void* x, const void*
     P6_CHECK_ARG(g.log2SC >= 0 && Cin % bk == 0, "pose6d_conv2d_fwd: Cin must be 4 or a power of two >= %d (got %d)",
                  bk, Cin);
   if (mode == kGemm) P6_CHECK_ARG(Cin % bk == 0, "pose6d_conv2d_fwd: 1x1 Cin %% %d != 0", bk);
+  if (mode == kFwdRowTap)
+    P6_CHECK_ARG(dtype == POSE6D_DT_F32 || W % 2 == 0, "pose6d_conv2d_fwd: the bf16 row-tap stem needs an even W");
   return run_conv(dtype, mode, g, x, w, bias, nullptr, y, stats, p6::stream_of(stream), tuning, true, splitk_ws,
                   splitk_ws_bytes);
+}
+
+extern "C" int pose6d_conv_pack_geom(int32_t dtype, int32_t Cin, int32_t KH, int32_t KW, int32_t stride, int32_t pad,
+                                     int32_t* kw_packed, int32_t* Kpad) {
+  P6_CHECK_ARG(kw_packed && Kpad && Cin > 0 && KH > 0 && KW > 0, "pose6d_conv_pack_geom: bad arguments");
+  *Kpad = pack_geom(dtype, Cin, KH, KW, stride, pad, kw_packed);
+  return POSE6D_OK;
 }
 
 // eval-mode conv + BatchNorm apply (+ residual, + ReLU) in one launch: the store of
@@ -1748,6 +1804,8 @@ extern "C" int pose6d_conv2d_fwd_act(int32_t dtype, const void* x, const void* w
     P6_CHECK_ARG(g.log2SC >= 0 && Cin % bk == 0,
                  "pose6d_conv2d_fwd_act: Cin must be 4 or a power of two >= %d (got %d)", bk, Cin);
   if (mode == kGemm) P6_CHECK_ARG(Cin % bk == 0, "pose6d_conv2d_fwd_act: 1x1 Cin %% %d != 0", bk);
+  P6_CHECK_ARG(mode != kFwdRowTap && mode != kFwdNarrow,
+               "pose6d_conv2d_fwd_act: 4-channel convs have no BN-act epilogue (pose6d_conv2d_fwd, then the BN)");
   g.act = 1;
   g.act_relu = relu != 0;
   g.act_scale = scale;

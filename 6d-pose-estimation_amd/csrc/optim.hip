@@ -293,10 +293,13 @@ __global__ __launch_bounds__(kThreads) void adamw_packed_kernel(float* __restric
 #define POSE6D_ADAMW_NOWT 0
 #endif
   if (taps > 1 && !POSE6D_ADAMW_NOWP) {
-    // wp[o][tap*Ip + c0 + ci], ci < cw: column ci*taps + tap of the tile
+    // wp[o][ptap*Ip + c0 + ci], ci < cw: column ci*taps + tap of the tile, at packed tap
+    // ptap = kh*KWp + kw + KWp - KW (KWp = KW but for the row-tap stems)
+    const int kwp = d.KWp > 0 ? d.KWp : d.KW;
     for (int it = tid; it < rows * taps; it += kThreads) {
       const int row = it / taps, tap = it - row * taps;
-      T* dst = wp + (int64_t)row * d.Kpad + tap * d.Ip + c0;
+      const int kh = tap / d.KW, ptap = tap + kh * (kwp - d.KW) + (kwp - d.KW);
+      T* dst = wp + (int64_t)row * d.Kpad + ptap * d.Ip + c0;
       const float* src = tile + row * LD + tap;
       if (cw == 8 && ((uintptr_t)dst & 15) == 0) {
         float x[8];
@@ -372,7 +375,8 @@ static int packed_jobs(const void* descs, int32_t n_desc, const float* param, in
     const int64_t off = d[k].w - param, len = (int64_t)d[k].O * d[k].I * d[k].KH * d[k].KW;
     P6_CHECK_ARG(d[k].w >= param && off + len <= n && (off & 3) == 0 && d[k].wp,
                  "pose6d_adamw_packed_jobs: conv %d's master is not a 16-B aligned slice of param", k);
-    P6_CHECK_ARG(d[k].Kpad >= d[k].KH * d[k].KW * d[k].Ip && d[k].Ip >= d[k].I && (d[k].Kpad & 3) == 0,
+    const int kwp = d[k].KWp > 0 ? d[k].KWp : d[k].KW;
+    P6_CHECK_ARG(kwp >= d[k].KW && d[k].Kpad >= d[k].KH * kwp * d[k].Ip && d[k].Ip >= d[k].I && (d[k].Kpad & 3) == 0,
                  "pose6d_adamw_packed_jobs: conv %d: bad packed geometry", k);
     reg.push_back({off, k});
   }

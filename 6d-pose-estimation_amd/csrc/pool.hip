@@ -111,7 +111,6 @@ __global__ __launch_bounds__(kThreads) void pack_kernel(const PackDesc* __restri
   const int R = d.I * taps;
   const int tid = threadIdx.x;
   if (blockIdx.z == 0) {
-    const int K = taps * d.Ip;
     if (taps == 1 && d.Ip == d.I && d.Kpad == d.I && (d.I & 7) == 0) {
       const int64_t n8 = (int64_t)d.O * d.I / 8;
       for (int64_t q = blockIdx.x * (int64_t)kThreads + tid; q < n8; q += (int64_t)gridDim.x * kThreads) {
@@ -126,6 +125,8 @@ __global__ __launch_bounds__(kThreads) void pack_kernel(const PackDesc* __restri
       return;
     }
     const bool vec = (R & 3) == 0 && R <= kPackRow;
+    const int kwp = d.KWp > 0 ? d.KWp : d.KW, shift = kwp - d.KW;   // packed taps per kernel row
+    const int Kp = d.KH * kwp * d.Ip;
     for (int o = blockIdx.x; o < d.O; o += gridDim.x) {
       const float* row = d.w + (int64_t)o * R;
       const bool staged = R <= kPackRow;
@@ -144,9 +145,11 @@ __global__ __launch_bounds__(kThreads) void pack_kernel(const PackDesc* __restri
         for (int h = 0; h < 2; ++h) {
           const int kk = k + h;
           v[h] = 0.f;
-          if (kk < K) {
-            const int tap = kk / d.Ip, c = kk - tap * d.Ip;
-            if (c < d.I) v[h] = staged ? sm[c * taps + tap] : row[c * taps + tap];
+          if (kk < Kp) {
+            const int pt = kk / d.Ip, c = kk - pt * d.Ip;
+            const int kh = pt / kwp, kw = pt - kh * kwp - shift;
+            const int tap = kh * d.KW + kw;
+            if (c < d.I && kw >= 0) v[h] = staged ? sm[c * taps + tap] : row[c * taps + tap];
           }
         }
         store2(dst + k, v[0], v[1]);

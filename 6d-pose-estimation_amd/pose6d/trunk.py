@@ -60,20 +60,30 @@ def _bn_stats(op):
 _FOLD = np.dtype([("gamma", "<u8"), ("beta", "<u8"), ("rmean", "<u8"), ("rvar", "<u8"), ("scale", "<u8"),
                   ("shift", "<u8"), ("smean", "<u8"), ("sinv", "<u8"), ("eps", "<f4"), ("C", "<i4")])
 _DESC = np.dtype([("w", "<u8"), ("wp", "<u8"), ("wt", "<u8"), ("O", "<i4"), ("I", "<i4"), ("Ip", "<i4"),
-                  ("KH", "<i4"), ("KW", "<i4"), ("Kpad", "<i4"), ("start", "<i8"), ("count", "<i8")])
+                  ("KH", "<i4"), ("KW", "<i4"), ("Kpad", "<i4"), ("KWp", "<i4"), ("reserved", "<i4"),
+                  ("start", "<i8")])
 
 
-def pack_single(w, cin_pad, dtype, with_t=True):
-    """Pack one OIHW fp32 device weight -> (wp [O][Kpad], wt [Ipad][KH][KW][O] or None)."""
+def pack_geom(dtype, cin_pad, k, stride, pad):
+    """(taps per packed kernel row, Kpad) of a forward filter (pose6d_conv_pack_geom)."""
+    kwp, kpad = ctypes.c_int32(), ctypes.c_int32()
+    call("conv_pack_geom", DTYPES[dtype], cin_pad, k, k, stride, pad, ctypes.byref(kwp),
+         ctypes.byref(kpad))
+    return kwp.value, kpad.value
+
+
+def pack_single(w, cin_pad, dtype, with_t=True, stride=1, pad=None):
+    """Pack one OIHW fp32 device weight -> (wp [O][Kpad], wt [Ipad][KH][KW][O] or None).
+    stride / pad (default: 'same' padding) select the forward layout (pose6d_conv_pack_geom:
+    the 4-channel 7x7 / stride-2 stems use the row-tap layout)."""
     O, I, KH, KW = w.shape
-    bk = 32 if dtype == torch.bfloat16 else 16
-    Kpad = (KH * KW * cin_pad + bk - 1) // bk * bk
+    kwp, Kpad = pack_geom(dtype, cin_pad, KH, stride, KH // 2 if pad is None else pad)
     wp = torch.empty(O, Kpad, device=w.device, dtype=dtype)
     wt = torch.empty(cin_pad, KH, KW, O, device=w.device, dtype=dtype) if with_t else None
     w = w.detach().float().contiguous()
     rec = np.zeros(1, _DESC)
-    rec[0] = (w.data_ptr(), wp.data_ptr(), wt.data_ptr() if wt is not None else 0, O, I, cin_pad, KH, KW, Kpad, 0,
-              O * Kpad)
+    rec[0] = (w.data_ptr(), wp.data_ptr(), wt.data_ptr() if wt is not None else 0, O, I, cin_pad, KH, KW, Kpad, kwp,
+              0, 0)
     d = torch.from_numpy(rec.view(np.uint8).copy()).to(w.device)
     call("pack_conv_weights", DTYPES[dtype], d, 1, O * Kpad, stream())
     torch.cuda.current_stream().synchronize()   # `d` / `w` are temporaries
@@ -227,9 +237,7 @@ class TrunkEngine:
             o.g = e(B, o.H, o.W, o.C)
             if isinstance(op, _ConvOp):
                 M = B * op.Ho * op.Wo
-                kp = op.k * op.k * op.cin_pad
-                bk = 32 if dtype == torch.bfloat16 else 16
-                op.Kpad = (kp + bk - 1) // bk * bk
+                op.KWp, op.Kpad = pack_geom(dtype, op.cin_pad, op.k, op.stride, op.pad)
                 op.wp = e(op.cout, op.Kpad)
                 op.wt = e(op.cin_pad, op.k, op.k, op.cout) if op.needs_dgrad else None
                 rows = query("conv_stats_rows", B, op.Ho, op.Wo, op.cout)
@@ -336,7 +344,7 @@ class TrunkEngine:
         for i, op in enumerate(self.convs):
             w = op.conv.weight
             rec[i] = (w.data_ptr(), op.wp.data_ptr(), op.wt.data_ptr() if op.wt is not None else 0, op.cout, op.cin,
-                      op.cin_pad, op.k, op.k, op.Kpad, start, op.cout * op.Kpad)
+                      op.cin_pad, op.k, op.k, op.Kpad, op.KWp, 0, start)
             start += op.cout * op.Kpad
         self._pack_total = start
         self._desc_host = rec   # (host copy: pose6d_adamw_packed_jobs reads it)

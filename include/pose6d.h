@@ -169,13 +169,20 @@ int pose6d_nchw_to_nhwc(int32_t dtype, const float *x, void *y, int32_t N, int32
                         int32_t Cpad, void *stream);
 
 /* One launch packs every conv's OIHW fp32 master weight into the kernel layouts:
- * wp [O][Kpad] (K = (kh, kw, ci), ci padded to Ip, zeros beyond K) and, when
- * non-null, wt [I][KH][KW][O] for the data gradient.  `descs` is a device array of
+ * wp [O][Kpad] (K = (kh, kw', ci): ci padded to Ip, KWp packed taps kw' per kernel
+ * row with filter tap kw at kw' = kw + KWp - KW, zeros elsewhere and beyond K) and,
+ * when non-null, wt [I][KH][KW][O] for the data gradient.  `descs` is a device array of
  * n_desc records of pose6d_pack_desc_size() bytes:
- *   { const float *w; void *wp; void *wt; int32 O, I, Ip, KH, KW, Kpad; int64 start, count; }
- * with start = running sum of O*Kpad, total = sum of O*Kpad. */
+ *   { const float *w; void *wp; void *wt; int32 O, I, Ip, KH, KW, Kpad, KWp, reserved; int64 start; }
+ * (start: the caller's bookkeeping, unused; total: sum of O*Kpad, unused).  KWp and
+ * Kpad of a forward conv come from pose6d_conv_pack_geom. */
 int pose6d_pack_desc_size(void);
 int pose6d_pack_conv_weights(int32_t dtype, const void *descs, int32_t n_desc, int64_t total, void *stream);
+/* Packed layout of a conv's forward filter (wp): taps per kernel row (*kw_packed: KW,
+ * or 8 for the row-tap stems -- Cin 4, stride 2, a kernel row of <= 8 taps: 7x7 / pad 3,
+ * read by the LDS-DMA kernel as 64-byte input rows) and the padded K (*Kpad). */
+int pose6d_conv_pack_geom(int32_t dtype, int32_t Cin, int32_t KH, int32_t KW, int32_t stride, int32_t pad,
+                          int32_t *kw_packed, int32_t *Kpad);
 
 /* nn.Conv2d forward (implicit GEMM on MFMA).  x [N][H][W][Cin] (Cin = 4 for the
  * padded stem, else a power of two), wp packed [Cout][Kpad], y [N][Ho][Wo][Cout].

@@ -38,7 +38,7 @@ def test_packed_jobs_cover_every_parameter_once():
     for i, (O, I, k) in enumerate(shapes):
         off = (off + 63) // 64 * 64
         ip = (I + 7) // 8 * 8
-        rec[i] = (base + 4 * off, 0x1000, 0, O, I, ip, k, k, (k * k * ip + 31) // 32 * 32, 0, 0)
+        rec[i] = (base + 4 * off, 0x1000, 0, O, I, ip, k, k, (k * k * ip + 31) // 32 * 32, k, 0, 0)
         offs.append((off, O * I * k * k))
         off += O * I * k * k + 37   # + a gap of plain parameters
     n = (off + 63) // 64 * 64
@@ -63,12 +63,12 @@ def test_packed_jobs_cover_every_parameter_once():
 def test_packed_jobs_reject_bad_tables():
     rec = np.zeros(2, dtype=_DESC)
     base = 1 << 20
-    rec[0] = (base, 0x1000, 0, 64, 64, 64, 1, 1, 64, 0, 0)
-    rec[1] = (base + 4 * 64, 0x1000, 0, 64, 64, 64, 1, 1, 64, 0, 0)   # overlaps conv 0
+    rec[0] = (base, 0x1000, 0, 64, 64, 64, 1, 1, 64, 1, 0, 0)
+    rec[1] = (base + 4 * 64, 0x1000, 0, 64, 64, 64, 1, 1, 64, 1, 0, 0)   # overlaps conv 0
     assert query("adamw_packed_jobs", rec.ctypes.data, 2, base, 1 << 16, None, 0) < 0
-    rec[1] = (base + 4 * 4098, 0x1000, 0, 64, 64, 64, 1, 1, 64, 0, 0)
+    rec[1] = (base + 4 * 4098, 0x1000, 0, 64, 64, 64, 1, 1, 64, 1, 0, 0)
     assert query("adamw_packed_jobs", rec.ctypes.data, 2, base, 8192, None, 0) < 0   # past the end
-    rec[1] = (base + 4 * 4097, 0x1000, 0, 64, 64, 64, 1, 1, 64, 0, 0)
+    rec[1] = (base + 4 * 4097, 0x1000, 0, 64, 64, 64, 1, 1, 64, 1, 0, 0)
     assert query("adamw_packed_jobs", rec.ctypes.data, 2, base, 1 << 16, None, 0) < 0   # misaligned
 
 

@@ -67,7 +67,7 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
     dev = "cuda"
     xd = _nhwc(x, cpad).to(dev, dtype)
     wd = w.to(dev)
-    wp, wt = pack_single(wd, cpad, dtype, with_t=Cin >= 8)
+    wp, wt = pack_single(wd, cpad, dtype, with_t=Cin >= 8, stride=s, pad=p)
     y = torch.empty(N, Ho, Wo, Cout, device=dev, dtype=dtype)
     rows = query("conv_stats_rows", N, Ho, Wo, Cout)
     stats = torch.empty(2, Cout, rows, device=dev)
@@ -758,18 +758,23 @@ def test_pools(dtype):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("O,I,k,cpad", [(64, 3, 7, 4), (256, 64, 1, 64), (64, 64, 3, 64), (512, 512, 3, 512),
-                                         (2048, 1024, 1, 1024), (100, 72, 3, 72)])
-def test_pack_layouts(dtype, O, I, k, cpad):
-    """pose6d_pack_conv_weights: wp[o][(kh, kw, ci)] with channel / K zero padding and
+@pytest.mark.parametrize("O,I,k,cpad,stride", [(64, 3, 7, 4, 1), (64, 3, 7, 4, 2), (32, 3, 7, 4, 2),
+                                                (256, 64, 1, 64, 1), (64, 64, 3, 64, 1), (512, 512, 3, 512, 1),
+                                                (2048, 1024, 1, 1024, 1), (100, 72, 3, 72, 2)])
+def test_pack_layouts(dtype, O, I, k, cpad, stride):
+    """pose6d_pack_conv_weights: wp[o][(kh, kw', ci)] with channel / K zero padding --
+    kw' = kw, or for the 4-channel stride-2 7x7 stems (pose6d_conv_pack_geom) the
+    row-tap layout, 8 taps per kernel row with a zero tap in front -- and
     wt[ci][kh][kw][o], exactly the dtype-rounded OIHW values."""
-    from pose6d.trunk import pack_single
+    from pose6d.trunk import pack_geom, pack_single
     g = torch.Generator(device="cuda").manual_seed(O + I + k)
     w = torch.randn(O, I, k, k, device="cuda", generator=g)
-    wp, wt = pack_single(w, cpad, dtype, with_t=I >= 8)
+    wp, wt = pack_single(w, cpad, dtype, with_t=I >= 8, stride=stride)
     torch.cuda.synchronize()
-    ref = torch.zeros(O, k, k, cpad, device="cuda")
-    ref[..., :I] = w.permute(0, 2, 3, 1)
+    kwp, _ = pack_geom(dtype, cpad, k, stride, k // 2)
+    assert kwp == (8 if (cpad == 4 and stride == 2 and k == 7) else k)
+    ref = torch.zeros(O, k, kwp, cpad, device="cuda")
+    ref[:, :, kwp - k:, :I] = w.permute(0, 2, 3, 1)
     ref = ref.reshape(O, -1)
     Kpad = wp.shape[1]
     full = torch.zeros(O, Kpad, device="cuda")

@@ -21,7 +21,7 @@ def main():
     Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
     x = torch.randn(B, H, W, Cin, device=dev).to(dtype)
     w = torch.randn(Cout, Cin, k, k, device=dev) * 0.05
-    wp, wt = pack_single(w, Cin, dtype)
+    wp, wt = pack_single(w, Cin, dtype, stride=s, pad=p)
     y = torch.empty(B, Ho, Wo, Cout, device=dev, dtype=dtype)
     dy = torch.randn(B, Ho, Wo, Cout, device=dev).to(dtype)
     dx = torch.empty(B, H, W, Cin, device=dev, dtype=dtype)
