@@ -77,6 +77,17 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
+// Row-tap layout (the 4-channel 7x7 / stride-2 stems): K ordered (kernel row, kRowTaps
+// taps, 4 channels) with the filter's KW taps at the END of each row of kRowTaps, so
+// that the taps of one kernel row of one output pixel are kRowTaps consecutive input
+// pixels starting at an even one (2 ox - pad - (kRowTaps - KW)): 64 / 128 contiguous
+// bytes (bf16 / fp32) per (pixel, kernel row).  Forward filters (wp) and the bf16
+// weight-gradient slabs use it for these convs.
+constexpr int kRowTaps = 8;
+__host__ __device__ inline bool rowtap_geom(int Cin, int KH, int KW, int stride, int pad) {
+  return Cin == 4 && stride == 2 && KH > 1 && KW <= kRowTaps && ((pad + kRowTaps - KW) & 1) == 0;
+}
+
 // one conv's weight-packing record (pose6d_pack_conv_weights, pose6d_adamw_step_packed)
 struct PackDesc {
   const float* w;   // OIHW fp32 master

@@ -41,15 +41,14 @@ template <> struct KT<float> { static constexpr int VEC = 4; static constexpr in
 // set; the epilogue applies both BatchNorms exactly as the separate launches did.
 enum Mode { kGemm = 0, kFwd = 1, kFwdNarrow = 2, kDgrad = 3, kDgradS2 = 4, kGemmDual = 5, kFwdRowTap = 6 };
 
-// Row-tap forward (kFwdRowTap: the 4-channel stems, 7x7 / stride 2 / pad 3): K is
-// ordered (kernel row kh, tap kw' = kw + 1 in 0..7, channel c), the filter packed with
-// kRowTaps taps per kernel row and a zero tap in front (pose6d_conv_pack_geom), so the
-// 8 taps x 4 channels of one kernel row of one output pixel are 8 consecutive input
-// pixels -- 64 contiguous bytes (bf16) starting at an even pixel (2 ox - pad - 1): the
-// LDS-DMA A tile fetches them as four aligned 16-B chunks (fp32: two kernel rows' worth
-// per 128-B K-step row becomes one row, 32 elements).  Replaces the register-staged
+// Row-tap forward (kFwdRowTap: the 4-channel stems, 7x7 / stride 2 / pad 3; layout in
+// common.h): the filter packed with kRowTaps taps per kernel row and a zero tap in front
+// (pose6d_conv_pack_geom), so the 8 taps x 4 channels of one kernel row of one output
+// pixel are 8 consecutive input pixels -- 64 contiguous bytes (bf16) starting at an
+// even pixel (2 ox - pad - 1): the LDS-DMA A tile fetches them as four aligned 16-B
+// chunks (fp32: one kernel row per 128-B K-step row).  Replaces the register-staged
 // 8-byte gather of kFwdNarrow for these convs.
-constexpr int kRowTaps = 8;
+using p6::kRowTaps;
 
 struct Geom {
   int M, Ncols, K, Kpad;   // GEMM dims; Kpad = weight row length
@@ -1710,8 +1709,7 @@ int run_conv(int dtype, int mode, const Geom& g, const void* src, const void* w,
 // kRowTaps for the row-tap stems) and the padded K, a multiple of the K-step of every
 // kernel that reads it.  pose6d_conv_pack_geom exports it.
 int pack_geom(int dtype, int Cin, int KH, int KW, int stride, int pad, int* kwp) {
-  // the first tap pixel 2 ox - pad - (kRowTaps - KW) is even (16-B aligned chunks)
-  const bool rowtap = Cin == 4 && stride == 2 && KH > 1 && KW <= kRowTaps && ((pad + kRowTaps - KW) & 1) == 0;
+  const bool rowtap = p6::rowtap_geom(Cin, KH, KW, stride, pad);
   *kwp = rowtap ? kRowTaps : KW;
   const int ks = dtype == POSE6D_DT_BF16 ? 64 : 32;   // LDS-DMA K-step
   const int bk = rowtap ? ks : (dtype == POSE6D_DT_BF16 ? 32 : 16);
@@ -2007,8 +2005,8 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
   const ReduceJob none{};
   auto flush_prev = [&]() -> int {   // the carried reduce as a launch of its own
     if (!rj || rj->nblk == 0) return POSE6D_OK;
-    return p6::wgrad_reduce_launch(rj->ws, rj->dw, rj->Cout, rj->Kpad, rj->SC, rj->Cin, rj->KH, rj->KW, rj->splits,
-                                   rj->accumulate, p6::stream_of(stream));
+    return p6::wgrad_reduce_launch(rj->ws, rj->dw, rj->Cout, rj->Kpad, rj->SC, rj->Cin, rj->KH, rj->KW, rj->KWp,
+                                   rj->splits, rj->accumulate, p6::stream_of(stream));
   };
   P6_CHECK_ARG(phases >= 1 && phases <= 3, "pose6d_conv2d_backward_ex: phases must be 1, 2 or 3");
   P6_CHECK_ARG(!bnr || (dx && phases == 3), "pose6d_conv2d_backward: a BatchNorm reduce needs the data gradient");
@@ -2020,7 +2018,9 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
     if (!deferred || phases != 3) return POSE6D_OK;
     p6::WgradPlan pw;
     const p6::WGeom gw = p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw, tn);
-    if (pw.fast && dtype == POSE6D_DT_BF16) return POSE6D_OK;   // bf16 LDS-DMA plans: the fused launch
+    // bf16 LDS-DMA plans go through the fused launch -- except a weight gradient alone
+    // (no data gradient: the row-tap stems), whose LDS-DMA kernel carries the reduce too
+    if (pw.fast && dtype == POSE6D_DT_BF16 && dx != nullptr) return POSE6D_OK;
     P6_CHECK_ARG((int64_t)pw.splits * Cout * gw.Kpad * 4 <= ws_bytes,
                  "pose6d_conv2d_backward: workspace %lld bytes < %lld needed", (long long)ws_bytes,
                  (long long)pw.splits * Cout * gw.Kpad * 4);
@@ -2109,7 +2109,8 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
     return rc;
   }
   if (rc || !(phases & 2)) return rc;
-  return p6::wgrad_reduce_launch(workspace, dw, Cout, gw.Kpad, Cin, Cin_real, KH, KW, gw.splits, accumulate, s);
+  return p6::wgrad_reduce_launch(workspace, dw, Cout, gw.Kpad, Cin, Cin_real, KH, KW, gw.kwp, gw.splits, accumulate,
+                                 s);
 }
 }  // namespace
 
@@ -2202,7 +2203,7 @@ ReduceJob make_job(const pose6d_wgrad_reduce_t& j) {
                                      &pw);
   ReduceJob r{};
   r.ws = j.ws; r.dw = j.dw; r.Cout = j.Cout; r.Kpad = g.Kpad; r.SC = j.Cin; r.Cin = j.Cin_real;
-  r.KH = j.KH; r.KW = j.KW; r.splits = g.splits; r.accumulate = j.accumulate;
+  r.KH = j.KH; r.KW = j.KW; r.KWp = g.kwp; r.splits = g.splits; r.accumulate = j.accumulate;
   r.G = reduce_group(g.splits);
   r.nblk = reduce_blocks(j.Cout, g.Kpad, r.G);
   return r;
@@ -2212,7 +2213,7 @@ ReduceJob make_job(const pose6d_wgrad_reduce_t& j) {
 extern "C" int pose6d_wgrad_reduce(const pose6d_wgrad_reduce_t* job, void* stream) {
   P6_CHECK_ARG(job != nullptr, "pose6d_wgrad_reduce: null job");
   const ReduceJob r = make_job(*job);
-  return p6::wgrad_reduce_launch(r.ws, r.dw, r.Cout, r.Kpad, r.SC, r.Cin, r.KH, r.KW, r.splits, r.accumulate,
+  return p6::wgrad_reduce_launch(r.ws, r.dw, r.Cout, r.Kpad, r.SC, r.Cin, r.KH, r.KW, r.KWp, r.splits, r.accumulate,
                                  p6::stream_of(stream));
 }
 

@@ -224,16 +224,17 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const T* __restric
 template <int G>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw,
                                                            int Cout, int Kpad, int SC, int Cin, int KH, int KW,
-                                                           int splits, int accumulate) {
+                                                           int KWp, int splits, int accumulate) {
   __shared__ float4 red[256];
-  wgrad_reduce_body<G>(red, blockIdx.x, ws, dw, Cout, Kpad, SC, Cin, KH, KW, splits, accumulate);
+  wgrad_reduce_body<G>(red, blockIdx.x, ws, dw, Cout, Kpad, SC, Cin, KH, KW, KWp, splits, accumulate);
 }
 
-int launch_reduce(const float* ws, float* dw, int Cout, int Kpad, int SC, int Cin, int KH, int KW, int splits,
-                  int accumulate, hipStream_t s) {
+int launch_reduce(const float* ws, float* dw, int Cout, int Kpad, int SC, int Cin, int KH, int KW, int KWp,
+                  int splits, int accumulate, hipStream_t s) {
   const int64_t quads = (int64_t)Cout * Kpad / 4;
   auto go = [&](auto kern, int L) {
-    kern<<<(unsigned)((quads + L - 1) / L), 256, 0, s>>>(ws, dw, Cout, Kpad, SC, Cin, KH, KW, splits, accumulate);
+    kern<<<(unsigned)((quads + L - 1) / L), 256, 0, s>>>(ws, dw, Cout, Kpad, SC, Cin, KH, KW, KWp, splits,
+                                                         accumulate);
   };
   if (splits >= 64) go(wgrad_reduce_kernel<16>, 16);
   else if (splits >= 16) go(wgrad_reduce_kernel<4>, 64);
@@ -244,12 +245,18 @@ int launch_reduce(const float* ws, float* dw, int Cout, int Kpad, int SC, int Ci
 
 using Plan = p6::WgradPlan;
 
-template <int S, bool PW>
+// trailing workgroups (rj.nblk) run a carried slab reduce of the previous conv
+template <int S, bool PW, bool RT>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_lds_kernel(const bf16* __restrict__ x,
                                                                   const bf16* __restrict__ dy,
-                                                                  float* __restrict__ ws, WGeom g) {
+                                                                  float* __restrict__ ws, WGeom g, ReduceJob rj) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv_wgrad_lds_body<64, 64, S, PW>(smem, blockIdx.x, x, dy, ws, g);
+  const int tiles = g.gm * g.gn;
+  if ((int)blockIdx.x >= tiles * g.splits) {
+    run_reduce_job(smem, blockIdx.x - tiles * g.splits, rj);
+    return;
+  }
+  conv_wgrad_lds_body<64, 64, S, PW, RT>(smem, blockIdx.x, x, dy, ws, g);
 }
 
 // fp32 LDS-DMA weight gradient (wgrad_body.h conv_wgrad_lds_body_f32); trailing
@@ -320,7 +327,11 @@ int tuned(const pose6d_tuning_t* t, int32_t pose6d_tuning_t::*f, int dflt) {
 
 // bf16 weight gradients take the LDS-DMA kernel (64x64 tiles, 3-slot ring) unless a
 // pose6d_tuning_t (tests / tools only) asks for the register-staged kernel or another ring
-Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* tn = nullptr) {
+// rowtap: the bf16 row-tap stem (wgrad_geom): SC is passed as 64 (its X image rows are
+// 64 K-elements by construction); it aims for ~4 workgroups per CU on a 2-slot ring --
+// its 4 K-tiles x 64 splits (one workgroup per CU, 98 64-pixel stages each) left each
+// workgroup waiting on its DMA: 56 -> 34 us graph-timed (profiles/r05w_stem_wgrad_sweep.txt)
+Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* tn = nullptr, bool rowtap = false) {
   Plan p{};
   // wgrad_base: 0 = default, 1 = register-staged; fp32 only: 2 = LDS-DMA 64x64 tiles,
   // 3 = LDS-DMA 128x128 tiles (each where the channel counts allow it, else the default)
@@ -364,6 +375,12 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
     // 4.64 / 4.70 / 4.65 / 4.65 / 4.71 / 4.81 / 4.89 ms per step (640 was the best
     // target while the data gradient went first: 5.14 ms then, 384 -> 5.24)
     target = Kpad == SC ? POSE6D_WGRAD_TARGET : POSE6D_WGRAD_TARGET_KXK;   // 1x1 / larger filters
+    if (rowtap) {
+      target = 1024;
+      p.stages = tuned(tn, &pose6d_tuning_t::wgrad_stages, 2);
+      if (p.stages < 2) p.stages = 2;
+      if (p.stages > 4) p.stages = 4;
+    }
     min_rows = 256;
     step = 64;
     max_bytes = 48ll << 20;
@@ -411,17 +428,26 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
 }
 
 template <int S>
-int launch_fast(const WGeom& g, const void* x, const void* dy, float* ws, hipStream_t s) {
+int launch_fast(const WGeom& g, const void* x, const void* dy, float* ws, hipStream_t s,
+                const ReduceJob& rj = ReduceJob{}) {
   static_assert(S * (64 + 64) * 128 >= acc_stage_bytes<64, 64>(), "ring too small to stage the tile");
   const int lds = S * (64 + 64) * 128;
-  if (g.KH == 1 && g.KW == 1 && g.stride == 1 && g.pad == 0)
-    conv_wgrad_lds_kernel<S, true><<<g.gm * g.gn * g.splits, kThreads, lds, s>>>((const bf16*)x, (const bf16*)dy, ws,
-                                                                                 g);
+  const int grid = g.gm * g.gn * g.splits + rj.nblk;
+  if (g.kwp == p6::kRowTaps && g.SC == 4)
+    conv_wgrad_lds_kernel<S, false, true><<<grid, kThreads, lds, s>>>((const bf16*)x, (const bf16*)dy, ws, g, rj);
+  else if (g.KH == 1 && g.KW == 1 && g.stride == 1 && g.pad == 0)
+    conv_wgrad_lds_kernel<S, true, false><<<grid, kThreads, lds, s>>>((const bf16*)x, (const bf16*)dy, ws, g, rj);
   else
-    conv_wgrad_lds_kernel<S, false><<<g.gm * g.gn * g.splits, kThreads, lds, s>>>((const bf16*)x, (const bf16*)dy,
-                                                                                  ws, g);
+    conv_wgrad_lds_kernel<S, false, false><<<grid, kThreads, lds, s>>>((const bf16*)x, (const bf16*)dy, ws, g, rj);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
+}
+
+int launch_fast_any(const Plan& p, const WGeom& g, const void* x, const void* dy, float* ws, hipStream_t s,
+                    const ReduceJob& rj = ReduceJob{}) {
+  return p.stages == 2 ? launch_fast<2>(g, x, dy, ws, s, rj)
+       : p.stages == 3 ? launch_fast<3>(g, x, dy, ws, s, rj)
+                       : launch_fast<4>(g, x, dy, ws, s, rj);
 }
 
 template <typename T, int BM, int BN>
@@ -457,9 +483,21 @@ extern "C" int64_t pose6d_conv2d_wgrad_workspace_tuned(int32_t dtype, int32_t N,
                                                        const pose6d_tuning_t* tuning) {
   const int bk = dtype == POSE6D_DT_BF16 ? 32 : 16;
   const int K = KH * KW * Cin;
-  const int Kpad = p6::ceil_div(K, bk) * bk;
-  const Plan p = plan(dtype, N * Ho * Wo, Cout, Kpad, Cin, tuning);
-  return (int64_t)p.splits * Cout * Kpad * 4;
+  int64_t need = 0;
+  {
+    const int Kpad = p6::ceil_div(K, bk) * bk;
+    const Plan p = plan(dtype, N * Ho * Wo, Cout, Kpad, Cin, tuning);
+    need = (int64_t)p.splits * Cout * Kpad * 4;
+  }
+  // (the stride / padding are not arguments: a 4-channel stem may take the row-tap plan,
+  // whose slabs are wider -- report the larger of the two)
+  if (dtype == POSE6D_DT_BF16 && Cin == 4 && KH > 1 && KW <= p6::kRowTaps && Cout % 64 == 0) {
+    const int Kpad = p6::ceil_div(KH * p6::kRowTaps * 4, 64) * 64;
+    const Plan p = plan(dtype, N * Ho * Wo, Cout, Kpad, 64, tuning, true);
+    const int64_t rt = (int64_t)p.splits * Cout * Kpad * 4;
+    if (rt > need) need = rt;
+  }
+  return need;
 }
 
 extern "C" int64_t pose6d_conv2d_wgrad_workspace(int32_t dtype, int32_t N, int32_t Ho, int32_t Wo, int32_t Cin,
@@ -476,6 +514,21 @@ WGeom wgrad_geom(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int 
   g.M = N * Ho * Wo; g.Cout = Cout; g.K = KH * KW * Cin; g.Kpad = ceil_div(g.K, bk) * bk;
   g.SH = H; g.SW = W; g.SC = Cin; g.log2SC = ilog2(Cin); g.RH = Ho; g.RW = Wo;
   g.KH = KH; g.KW = KW; g.stride = stride; g.pad = pad;
+  g.kwp = KW;
+  // the bf16 4-channel stems: the LDS-DMA body on the row-tap X image (common.h), slabs in
+  // row-tap K order (64-column blocks = two kernel rows); the reduce maps them to OIHW
+  if (dtype == POSE6D_DT_BF16 && rowtap_geom(Cin, KH, KW, stride, pad) && Cout % 64 == 0 && (W & 1) == 0) {
+    const int Kpad = ceil_div(KH * kRowTaps * 4, 64) * 64;
+    const Plan p = plan(dtype, g.M, Cout, Kpad, 64, tuning, true);   // (64: the LDS-DMA channel rule holds)
+    if (p.fast) {
+      g.kwp = kRowTaps;
+      g.K = g.Kpad = Kpad;
+      g.gm = ceil_div(Cout, p.bm); g.gn = ceil_div(g.Kpad, p.bn);
+      g.splits = p.splits; g.mps = p.mps;
+      if (plan_out) *plan_out = p;
+      return g;
+    }
+  }
   const Plan p = plan(dtype, g.M, Cout, g.Kpad, Cin, tuning);
   g.gm = ceil_div(Cout, p.bm); g.gn = ceil_div(g.Kpad, p.bn);
   g.splits = p.splits; g.mps = p.mps;
@@ -483,14 +536,14 @@ WGeom wgrad_geom(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int 
   return g;
 }
 
-int wgrad_reduce_launch(const float* ws, float* dw, int Cout, int Kpad, int SC, int Cin, int KH, int KW, int splits,
-                        int accumulate, hipStream_t s) {
-  return launch_reduce(ws, dw, Cout, Kpad, SC, Cin, KH, KW, splits, accumulate, s);
+int wgrad_reduce_launch(const float* ws, float* dw, int Cout, int Kpad, int SC, int Cin, int KH, int KW, int KWp,
+                        int splits, int accumulate, hipStream_t s) {
+  return launch_reduce(ws, dw, Cout, Kpad, SC, Cin, KH, KW, KWp, splits, accumulate, s);
 }
 
 int wgrad_launch_carry(int dtype, const WGeom& g, const WgradPlan& p, const void* x, const void* dy, float* ws,
                        const ReduceJob& rj, hipStream_t s) {
-  P6_CHECK_ARG(!p.fast || dtype == POSE6D_DT_F32, "wgrad_launch_carry: register-staged or fp32 plans only");
+  if (p.fast && dtype == POSE6D_DT_BF16) return launch_fast_any(p, g, x, dy, ws, s, rj);
   if (p.fast) return launch_fast_f32_any(p, g, x, dy, ws, s, rj);
   return dtype == POSE6D_DT_BF16 ? launch_any<bf16>(g, p.bm, p.bn, x, dy, ws, s, rj)
                                  : launch_any<float>(g, p.bm, p.bn, x, dy, ws, s, rj);
@@ -524,15 +577,13 @@ extern "C" int pose6d_conv2d_wgrad_tuned(int32_t dtype, const void* x, const voi
   if (p.fast && dtype == POSE6D_DT_F32) {
     rc = launch_fast_f32_any(p, g, x, dy, workspace, s, ReduceJob{});
   } else if (p.fast) {
-    rc = p.stages == 2 ? launch_fast<2>(g, x, dy, workspace, s)
-       : p.stages == 3 ? launch_fast<3>(g, x, dy, workspace, s)
-                       : launch_fast<4>(g, x, dy, workspace, s);
+    rc = launch_fast_any(p, g, x, dy, workspace, s);
   } else {
     rc = dtype == POSE6D_DT_BF16 ? launch_any<bf16>(g, p.bm, p.bn, x, dy, workspace, s)
                                  : launch_any<float>(g, p.bm, p.bn, x, dy, workspace, s);
   }
   if (rc) return rc;
-  return launch_reduce(workspace, dw, Cout, g.Kpad, Cin, Cin_real, KH, KW, g.splits, accumulate, s);
+  return launch_reduce(workspace, dw, Cout, g.Kpad, Cin, Cin_real, KH, KW, g.kwp, g.splits, accumulate, s);
 }
 
 // weight-gradient kernel variant: (stages << 12) | (fast << 8) | (BM == 128) << 1 | (BN == 128)

@@ -24,6 +24,7 @@ struct WGeom {
   int RH, RW;
   int KH, KW, stride, pad;
   int gm, gn, splits, mps;  // tiles over Cout, over K; splits; m per split (multiple of the step)
+  int kwp;                  // taps per kernel row of the slab's K order: KW, or kRowTaps (bf16 row-tap stems)
 };
 
 struct WgradPlan {
@@ -36,13 +37,14 @@ struct WgradPlan {
 struct ReduceJob {
   const float* ws;
   float* dw;
-  int Cout, Kpad, SC, Cin, KH, KW, splits, accumulate, G, nblk;
+  int Cout, Kpad, SC, Cin, KH, KW, KWp, splits, accumulate, G, nblk;
 };
 
 // defined in conv_wgrad.hip
 WGeom wgrad_geom(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad, int Ho,
                  int Wo, WgradPlan* plan, const pose6d_tuning_t* tuning = nullptr);
-int wgrad_reduce_launch(const float* ws, float* dw, int Cout, int Kpad, int SC, int Cin, int KH, int KW, int splits,
+int wgrad_reduce_launch(const float* ws, float* dw, int Cout, int Kpad, int SC, int Cin, int KH, int KW, int KWp,
+                        int splits,
                         int accumulate, hipStream_t s);
 // the register-staged weight gradient of plan `p` (not p.fast) with the carried
 // reduce `rj` as its trailing workgroups; its own slabs are left for the caller to
@@ -150,7 +152,10 @@ __device__ __forceinline__ void lds_wait_tr8(u32x2 (&f)[8]) {
 // pointer increment and one compare per row instead of the general (n, oy, ox)
 // walk with per-row padding checks (which left the 1x1 weight gradients issue
 // bound: ~1200 issue cycles per wave per K-step against 128 of MFMA)
-template <int BM, int BN, int S, bool PW = false>
+// RT: the row-tap X image (the 4-channel 7x7 / stride-2 stems, common.h): sub-image
+// s of a stage is the slab's K columns [k0 + 64 s, + 64) = two kernel rows x 8 taps x 4
+// channels, i.e. each X row is two 64-byte runs of 8 input pixels
+template <int BM, int BN, int S, bool PW = false, bool RT = false>
 __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const bf16* __restrict__ x,
                                                     const bf16* __restrict__ dy, float* __restrict__ ws,
                                                     const p6::WGeom& g) {
@@ -266,7 +271,13 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
 #pragma unroll
       for (int s = 0; s < XS; ++s) {
         const void* p = zp;
-        if (pointwise) {
+        if constexpr (RT) {
+          // this lane's chunk (8 elements = 2 taps x 4 channels) of K column block s
+          const int ke = k0 + s * 64 + ck[i];
+          const int kr = ke >> 5, yy = sy + kr, xx = sx - (p6::kRowTaps - g.KW) + ((ke & 31) >> 2);
+          if (ok && kr < g.KH && (unsigned)yy < (unsigned)g.SH && (unsigned)xx < (unsigned)g.SW)
+            p = x + ((((int64_t)rn[i] * g.SH + yy) * g.SW + xx) << 2);
+        } else if (pointwise) {
           if (ok) p = x + ((int64_t)m << g.log2SC) + ci0[s] + ck[i];
         } else {
           const int yy = sy + tap_h[s], xx = sx + tap_w[s];
@@ -562,7 +573,7 @@ __device__ __forceinline__ void conv_wgrad_lds_body_f32(char* smem, int bid, con
 template <int G>
 __device__ __forceinline__ void wgrad_reduce_body(float4* red, int blk, const float* __restrict__ ws,
                                                   float* __restrict__ dw, int Cout, int Kpad, int SC, int Cin, int KH,
-                                                  int KW, int splits, int accumulate) {
+                                                  int KW, int KWp, int splits, int accumulate) {
   constexpr int L = 256 / G;
   constexpr int U = 4;
   const int lane = threadIdx.x % L, grp = threadIdx.x / L;
@@ -600,14 +611,17 @@ __device__ __forceinline__ void wgrad_reduce_body(float4* red, int blk, const fl
     for (int g = 1; g < G; ++g) { const float4 v = red[g * L + lane]; t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w; }
     const float tv[4] = {t.x, t.y, t.z, t.w};
     const int co = (int)(e0 / Kpad), k0 = (int)(e0 - (int64_t)co * Kpad);
-    const int K = KH * KW * SC;
+    // slab K order (kh, kw', ci) with KWp taps kw' per kernel row, filter tap kw = kw' - (KWp - KW)
+    const int kwp = KWp > 0 ? KWp : KW;
+    const int K = KH * kwp * SC;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int k = k0 + j;
       if (k >= K) continue;
       const int tap = k / SC, ci = k - tap * SC;
       if (ci >= Cin) continue;
-      const int kh = tap / KW, kw = tap - kh * KW;
+      const int kh = tap / kwp, kw = tap - kh * kwp - (kwp - KW);
+      if (kw < 0) continue;
       float* d = dw + (((int64_t)co * Cin + ci) * KH + kh) * KW + kw;
       *d = accumulate ? *d + tv[j] : tv[j];
     }
@@ -625,11 +639,12 @@ __host__ __device__ inline int reduce_blocks(int Cout, int Kpad, int G) {
 
 __device__ __forceinline__ void run_reduce_job(char* smem, int blk, const ReduceJob& j) {
   float4* red = reinterpret_cast<float4*>(smem);
-  if (j.G == 16) wgrad_reduce_body<16>(red, blk, j.ws, j.dw, j.Cout, j.Kpad, j.SC, j.Cin, j.KH, j.KW, j.splits,
+  if (j.G == 16) wgrad_reduce_body<16>(red, blk, j.ws, j.dw, j.Cout, j.Kpad, j.SC, j.Cin, j.KH, j.KW, j.KWp, j.splits,
                                        j.accumulate);
-  else if (j.G == 4) wgrad_reduce_body<4>(red, blk, j.ws, j.dw, j.Cout, j.Kpad, j.SC, j.Cin, j.KH, j.KW, j.splits,
-                                          j.accumulate);
-  else wgrad_reduce_body<1>(red, blk, j.ws, j.dw, j.Cout, j.Kpad, j.SC, j.Cin, j.KH, j.KW, j.splits, j.accumulate);
+  else if (j.G == 4) wgrad_reduce_body<4>(red, blk, j.ws, j.dw, j.Cout, j.Kpad, j.SC, j.Cin, j.KH, j.KW, j.KWp,
+                                          j.splits, j.accumulate);
+  else wgrad_reduce_body<1>(red, blk, j.ws, j.dw, j.Cout, j.Kpad, j.SC, j.Cin, j.KH, j.KW, j.KWp, j.splits,
+                            j.accumulate);
 }
 
 }  // namespace

@@ -709,6 +709,65 @@ def test_wgrad_fast_vs_register_staged(dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [(2, 32, 32, 3, 64), (4, 224, 224, 3, 64), (2, 30, 26, 3, 128)])
+def test_stem_wgrad_rowtap(cfg):
+    """The bf16 4-channel 7x7 / stride-2 stem's weight gradient on the LDS-DMA body with
+    the row-tap X image (slabs in (kernel row, 8 taps, channel) order, mapped back to OIHW
+    by the reduce): against the float64 torch op on the same bf16 operands, and against
+    the register-staged kernel (Tuning(wgrad_base=1)); written and accumulated, standalone
+    and in chain mode (pose6d_conv2d_backward_chain without a data gradient, carrying a
+    previous conv's pending slab reduce and leaving its own pending)."""
+    import ctypes
+    from pose6d._lib import Tuning, call, query, stream
+    from pose6d.trunk import DTYPES, _WgradReduce
+    N, H, W, Cin, Cout = cfg
+    k, s, p, cp = 7, 2, 3, 4
+    dtype, dev = torch.bfloat16, "cuda"
+    dt = DTYPES[dtype]
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    g = torch.Generator().manual_seed(N + H + Cout)
+    x = torch.randn(N, Cin, H, W, generator=g).bfloat16().float()
+    dyt = torch.randn(N, Cout, Ho, Wo, generator=g).bfloat16().float()
+    ref = torch.nn.grad.conv2d_weight(x.double(), (Cout, Cin, k, k), dyt.double(), stride=s, padding=p)
+    xd, dyd = _nhwc(x, cp).to(dev, dtype), _nhwc(dyt).to(dev, dtype)
+    outs = []
+    for tn in (Tuning(), Tuning(wgrad_base=1)):
+        ws = torch.empty(query("conv2d_wgrad_workspace_tuned", dt, N, Ho, Wo, cp, Cout, k, k, tn.ref) // 4 + 1,
+                         device=dev)
+        dw = torch.full((Cout, Cin, k, k), 0.5, device=dev)
+        call("conv2d_wgrad_tuned", dt, xd, dyd, dw, 1, ws, ws.numel() * 4, N, H, W, cp, Cin, Cout, k, k, s, p,
+             Ho, Wo, tn.ref, stream())
+        torch.cuda.synchronize()
+        outs.append(dw.cpu() - 0.5)
+    for i, o in enumerate(outs):
+        _close(o, ref.float(), 1e-4, f"stem wgrad plan {i} {cfg}")
+    # chain mode: a previous (1x1) conv's pending reduce rides on the stem's launch
+    N2, C2 = 2, 64
+    x2 = torch.randn(N2, 8, 8, C2, generator=g).to(dev, dtype)
+    dy2 = torch.randn(N2, 8, 8, C2, generator=g).to(dev, dtype)
+    ws2 = torch.zeros(query("conv2d_wgrad_workspace", dt, N2, 8, 8, C2, C2, 1, 1) // 4 + 1, device=dev)
+    dw2 = torch.zeros(C2, C2, 1, 1, device=dev)
+    dx2 = torch.empty(N2, 8, 8, C2, device=dev, dtype=dtype)
+    deferred = ctypes.c_int32(0)
+    wt2 = torch.zeros(C2, 1, 1, C2, device=dev, dtype=dtype)
+    call("conv2d_backward_chain", dt, x2, dy2, wt2, None, dx2, dw2, 0, ws2, ws2.numel() * 4, N2, 8, 8, C2, C2, C2, 1,
+         1, 1, 0, 8, 8, None, ctypes.addressof(deferred), stream())
+    prev = _WgradReduce(ws2.data_ptr(), dw2.data_ptr(), dt, N2, 8, 8, C2, C2, C2, 1, 1, 1, 0, 8, 8, 0)
+    ws = torch.empty(query("conv2d_wgrad_workspace", dt, N, Ho, Wo, cp, Cout, k, k) // 4 + 1, device=dev)
+    dw = torch.zeros(Cout, Cin, k, k, device=dev)
+    d2 = ctypes.c_int32(0)
+    call("conv2d_backward_chain", dt, xd, dyd, None, None, None, dw, 0, ws, ws.numel() * 4, N, H, W, cp, Cin, Cout,
+         k, k, s, p, Ho, Wo, ctypes.addressof(prev) if deferred.value else None, ctypes.addressof(d2), stream())
+    if d2.value:
+        job = _WgradReduce(ws.data_ptr(), dw.data_ptr(), dt, N, H, W, cp, Cin, Cout, k, k, s, p, Ho, Wo, 0)
+        call("wgrad_reduce", ctypes.addressof(job), stream())
+    torch.cuda.synchronize()
+    _close(dw.cpu(), ref.float(), 1e-4, f"stem wgrad chain {cfg}")
+    ref2 = torch.einsum("nhwc,nhwd->dc", x2.double().cpu(), dy2.double().cpu()).reshape(C2, C2, 1, 1)
+    _close(dw2.cpu(), ref2.float(), 1e-4, "carried 1x1 reduce")
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_pools(dtype):
     from pose6d._lib import call, stream

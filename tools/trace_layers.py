@@ -18,11 +18,15 @@ def main():
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     marks = [i for i, r in enumerate(rows) if "pinhole_z_fwd_kernel" in r["Kernel_Name"]]
     win = rows[marks[-2] + 1:marks[-1]]
-    # last step: from the last pack_kernel on
+    # the last step of the window
     packs = [i for i, r in enumerate(win) if "pack_kernel" in r["Kernel_Name"]]
-    step = win[packs[-1]:]
+    if packs:   # (rounds <= 4: the step opened with the weight-packing launch)
+        step = win[packs[-1]:]
+    else:       # since round 5 the step ends with the AdamW launch that packs the weights
+        opt = [i for i, r in enumerate(win) if "adamw" in r["Kernel_Name"]]
+        step = win[opt[-2] + 1:opt[-1] + 1]
     conv = [r for r in step if any(k in r["Kernel_Name"] for k in ("conv_lds", "conv_igemm", "conv_bwd",
-                                                                    "conv_wgrad_kernel"))]
+                                                                    "conv_wgrad_kernel", "conv_wgrad_lds"))]
     convs = resnet50_convs()
     B = 32
     fwd = conv[:len(convs)]

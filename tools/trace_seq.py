@@ -18,7 +18,11 @@ def main():
     marks = [i for i, r in enumerate(rows) if "pinhole_z_fwd_kernel" in r["Kernel_Name"]]
     win = rows[marks[-2] + 1:marks[-1]]
     packs = [i for i, r in enumerate(win) if "pack_kernel" in r["Kernel_Name"]]
-    step = win[packs[-1]:]
+    if packs:   # (rounds <= 4: the step opened with the weight-packing launch)
+        step = win[packs[-1]:]
+    else:       # since round 5 the step ends with the AdamW launch that packs the weights
+        opt = [i for i, r in enumerate(win) if "adamw" in r["Kernel_Name"]]
+        step = win[opt[-2] + 1:opt[-1] + 1]
     for i, r in enumerate(step):
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3
         print(f"{i:4d} {d:8.1f} {short(r['Kernel_Name'])} grid={r.get('Grid_Size', '')}")
