@@ -34,12 +34,18 @@ def main():
     ap.add_argument("--model", default="rgbd_geometric")
     ap.add_argument("--eager", action="store_true", help="no hipGraph (PMC counter passes)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--attr", default="", help="module.Class.attribute=0|1 set before the trainer is built")
     a = ap.parse_args()
     from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
     from pose6d.train import RGBDGeometricTrainer
     torch.manual_seed(0)
     dev = torch.device("cuda", 0)
     model = PoseNetRGBDGeometric(pretrained=False).to(dev)
+    if a.attr:
+        import importlib
+        path, val = a.attr.split("=")
+        mod, cls, attr = path.rsplit(".", 2)
+        setattr(getattr(importlib.import_module(mod), cls), attr, bool(int(val)))
     tr = RGBDGeometricTrainer(model, 32, dtype=torch.bfloat16 if a.dtype == "bf16" else torch.float32)
     data = synth_batch(32, dev, seed=1000)
     if not a.eager:
