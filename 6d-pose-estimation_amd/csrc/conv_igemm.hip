@@ -2265,31 +2265,6 @@ extern "C" int pose6d_conv2d_backward_bn_rows(int32_t dtype, int32_t N, int32_t 
   return bnr_plan_rows(bwd_fused(dtype, pd, pw, nullptr) ? pd : choose(dtype, mode, gd0, false));
 }
 
-// the data gradient of pose6d_conv2d_backward_chain* alone: where that call runs the
-// fused launch, the same plan as its data-gradient role (64x64 tiles, its ring, no split)
-// -- the same bits and BN-reduce rows (pose6d_conv2d_backward_bn_rows)
-extern "C" int pose6d_conv2d_dgrad_ex(int32_t dtype, const void* dy, const void* wt, const void* dres,
-                                      const uint8_t* dres_mask, void* dx, int32_t N, int32_t H, int32_t W, int32_t Cin,
-                                      int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho,
-                                      int32_t Wo, const pose6d_bn_reduce_t* bn, void* stream) {
-  P6_CHECK_ARG(Cin % 8 == 0 && ilog2(Cin) >= 3, "pose6d_conv2d_dgrad_ex: Cin must be a power of two >= 8");
-  int mode;
-  const Geom gd0 = dgrad_geom(N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &mode);
-  const Plan pd = choose(dtype, mode, gd0, true);
-  p6::WgradPlan pw;
-  p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
-  pose6d_tuning_t t;
-  memset(&t, 0xff, sizeof t);   // every field -1 (default)
-  const bool fused = bwd_fused(dtype, pd, pw, nullptr);
-  if (fused) {
-    t.conv_tile = 3;
-    t.conv_stages = pd.stages;
-    t.conv_splitk = 1;
-  }
-  return dgrad_impl(dtype, dy, wt, dres, dres_mask, dx, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, stream,
-                    fused ? &t : nullptr, bn);
-}
-
 extern "C" int pose6d_conv2d_backward_chain_bn(int32_t dtype, const void* x, const void* dy, const void* wt,
                                                const void* dres, const uint8_t* dres_mask, void* dx, float* dw,
                                                int32_t accumulate, float* workspace, int64_t ws_bytes, int32_t N,

@@ -592,120 +592,3 @@ extern "C" int pose6d_wgrad_variant(int32_t dtype, int32_t M, int32_t Cout, int3
   const Plan p = plan(dtype, M, Cout, p6::ceil_div(K, bk) * bk, Cin);
   return (p.stages << 12) | ((int)p.fast << 8) | ((p.bm == 128) << 1) | (p.bn == 128);
 }
-
-// ----------------------------------------------------------------------------
-// Batched weight gradients (pose6d_conv2d_wgrad_batch): the LDS-DMA weight-gradient
-// workgroups of several convs in one launch (each conv its own plan, slabs and XCD
-// remap: its workgroup range starts at a multiple of 8), then all their slab reduces
-// in one more launch.  A weight gradient feeds only the optimizer, so the trainer can
-// take them off the data-gradient chain and run them here together, with far more
-// workgroups in flight than one conv's launch has.
-// ----------------------------------------------------------------------------
-namespace {
-
-struct BatchJob {
-  const bf16* x;
-  const bf16* dy;
-  float* ws;
-  WGeom g;
-  int wg0;   // first workgroup of this job
-  int pw, rt;
-};
-struct WgradBatch {
-  BatchJob j[POSE6D_WGRAD_BATCH_MAX];
-  int n;
-};
-struct RedBatch {
-  ReduceJob j[POSE6D_WGRAD_BATCH_MAX];
-  int blk0[POSE6D_WGRAD_BATCH_MAX];
-  int n;
-};
-constexpr int kBatchStages = 3;
-
-__global__ __launch_bounds__(kThreads) void wgrad_batch_kernel(const WgradBatch b) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  int j = 0;
-  while (j + 1 < b.n && (int)blockIdx.x >= b.j[j + 1].wg0) ++j;
-  const BatchJob& J = b.j[j];
-  const int bid = (int)blockIdx.x - J.wg0;
-  if (bid >= J.g.gm * J.g.gn * J.g.splits) return;   // the padding to a multiple of 8
-  if (J.rt) conv_wgrad_lds_body<64, 64, kBatchStages, false, true>(smem, bid, J.x, J.dy, J.ws, J.g);
-  else if (J.pw) conv_wgrad_lds_body<64, 64, kBatchStages, true, false>(smem, bid, J.x, J.dy, J.ws, J.g);
-  else conv_wgrad_lds_body<64, 64, kBatchStages, false, false>(smem, bid, J.x, J.dy, J.ws, J.g);
-}
-
-__global__ __launch_bounds__(256) void wgrad_reduce_batch_kernel(const RedBatch r) {
-  __shared__ float4 red[256];
-  int j = 0;
-  while (j + 1 < r.n && (int)blockIdx.x >= r.blk0[j + 1]) ++j;
-  run_reduce_job(reinterpret_cast<char*>(red), (int)blockIdx.x - r.blk0[j], r.j[j]);
-}
-
-}  // namespace
-
-extern "C" int pose6d_conv2d_wgrad_batch(int32_t dtype, const pose6d_wgrad_job_t* jobs, int32_t n, void* stream) {
-  P6_CHECK_ARG(dtype == POSE6D_DT_BF16, "pose6d_conv2d_wgrad_batch: bf16 only");
-  P6_CHECK_ARG(n >= 0 && n <= POSE6D_WGRAD_BATCH_MAX && (n == 0 || jobs), "pose6d_conv2d_wgrad_batch: bad job list");
-  hipStream_t s = p6::stream_of(stream);
-  WgradBatch b{};
-  RedBatch r{};
-  WGeom geo[POSE6D_WGRAD_BATCH_MAX];
-  Plan pl[POSE6D_WGRAD_BATCH_MAX];
-  int order[POSE6D_WGRAD_BATCH_MAX], m = 0;
-  for (int i = 0; i < n; ++i) {
-    const pose6d_wgrad_job_t& J = jobs[i];
-    P6_CHECK_ARG(ilog2(J.Cin) >= 2 && J.Cout % 8 == 0 && J.Cin_real <= J.Cin,
-                 "pose6d_conv2d_wgrad_batch: job %d: Cin must be a power of two >= 4", i);
-    geo[i] = p6::wgrad_geom(dtype, J.N, J.H, J.W, J.Cin, J.Cout, J.KH, J.KW, J.stride, J.pad, J.Ho, J.Wo, &pl[i]);
-    if (!pl[i].fast) {   // a register-staged plan: on its own (same bits as pose6d_conv2d_wgrad)
-      const int rc = pose6d_conv2d_wgrad_tuned(dtype, J.x, J.dy, J.dw, J.accumulate, J.ws, J.ws_bytes, J.N, J.H, J.W,
-                                               J.Cin, J.Cin_real, J.Cout, J.KH, J.KW, J.stride, J.pad, J.Ho, J.Wo,
-                                               nullptr, stream);
-      if (rc) return rc;
-      continue;
-    }
-    order[m++] = i;
-  }
-  // longest workgroups (most 64-pixel stages per split) first
-  for (int a = 1; a < m; ++a)
-    for (int c = a; c > 0 && geo[order[c]].mps > geo[order[c - 1]].mps; --c) {
-      const int t = order[c]; order[c] = order[c - 1]; order[c - 1] = t;
-    }
-  int wg = 0, blk = 0;
-  for (int q = 0; q < m; ++q) {
-    const int i = order[q];
-    const pose6d_wgrad_job_t& J = jobs[i];
-    const WGeom& g = geo[i];
-    // one split of a 1x1 conv whose K is exactly Cin: the slab IS the OIHW gradient
-    const bool direct = g.splits == 1 && J.KH == 1 && J.KW == 1 && g.Kpad == J.Cin && J.Cin_real == J.Cin &&
-                        !J.accumulate && g.kwp == J.KW;
-    if (!direct)
-      P6_CHECK_ARG(J.ws && J.ws_bytes >= (int64_t)g.splits * J.Cout * g.Kpad * 4,
-                   "pose6d_conv2d_wgrad_batch: job %d: workspace %lld bytes < %lld", i, (long long)J.ws_bytes,
-                   (long long)g.splits * J.Cout * g.Kpad * 4);
-    BatchJob& B = b.j[b.n++];
-    B.x = (const bf16*)J.x; B.dy = (const bf16*)J.dy; B.ws = direct ? J.dw : J.ws; B.g = g; B.wg0 = wg;
-    B.pw = J.KH == 1 && J.KW == 1 && J.stride == 1 && J.pad == 0;
-    B.rt = g.kwp == p6::kRowTaps && g.SC == 4;
-    wg += (g.gm * g.gn * g.splits + 7) / 8 * 8;
-    if (!direct) {
-      ReduceJob& R = r.j[r.n];
-      R.ws = J.ws; R.dw = J.dw; R.Cout = J.Cout; R.Kpad = g.Kpad; R.SC = J.Cin; R.Cin = J.Cin_real;
-      R.KH = J.KH; R.KW = J.KW; R.KWp = g.kwp; R.splits = g.splits; R.accumulate = J.accumulate;
-      R.G = reduce_group(g.splits);
-      R.nblk = reduce_blocks(J.Cout, g.Kpad, R.G);
-      r.blk0[r.n++] = blk;
-      blk += R.nblk;
-    }
-  }
-  if (wg == 0) return POSE6D_OK;
-  constexpr int lds = kBatchStages * (64 + 64) * 128;
-  static_assert(lds >= acc_stage_bytes<64, 64>(), "ring too small to stage the tile");
-  wgrad_batch_kernel<<<wg, kThreads, lds, s>>>(b);
-  P6_LAUNCH_CHECK();
-  if (r.n) {
-    wgrad_reduce_batch_kernel<<<blk, 256, 0, s>>>(r);
-    P6_LAUNCH_CHECK();
-  }
-  return POSE6D_OK;
-}

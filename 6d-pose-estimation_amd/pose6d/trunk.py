@@ -33,17 +33,6 @@ class _WgradReduce(ctypes.Structure):
                                       "Ho", "Wo", "accumulate")]
 
 
-class _WgradJob(ctypes.Structure):
-    """pose6d_wgrad_job_t (include/pose6d.h): one conv of pose6d_conv2d_wgrad_batch."""
-    _fields_ = [("x", ctypes.c_void_p), ("dy", ctypes.c_void_p), ("dw", ctypes.c_void_p), ("ws", ctypes.c_void_p),
-                ("ws_bytes", ctypes.c_int64)] + [
-        (n, ctypes.c_int32) for n in ("N", "H", "W", "Cin", "Cin_real", "Cout", "KH", "KW", "stride", "pad", "Ho",
-                                      "Wo", "accumulate")]
-
-
-WGRAD_BATCH_MAX = 24   # POSE6D_WGRAD_BATCH_MAX
-
-
 class _BnReduce(ctypes.Structure):
     """pose6d_bn_reduce_t (include/pose6d.h): the BN whose backward sums a data
     gradient's epilogue accumulates."""
@@ -546,21 +535,6 @@ class TrunkEngine:
             if on_conv_done is not None:
                 on_conv_done(o)
 
-        # deferred weight gradients (bf16): each conv launches its data gradient alone and
-        # its weight gradient joins a batch (pose6d_conv2d_wgrad_batch) that runs the
-        # weight gradients of up to WGRAD_BATCH_MAX convs together, off the data-gradient chain
-        defer = self.defer_wgrad and dt == DT_BF16
-        batch = []
-
-        def flush_batch():
-            if not batch:
-                return
-            jobs = (_WgradJob * len(batch))(*[j for j, _ in batch])
-            call("conv2d_wgrad_batch", dt, ctypes.addressof(jobs), len(batch), st)
-            for _, o in batch:
-                conv_done(o)
-            batch.clear()
-
         for op in reversed(self.ops):
             if isinstance(op, _ActOp):
                 c = op.cop
@@ -632,19 +606,6 @@ class TrunkEngine:
                         dx = src.g
                 if op.conv.bias is not None:   # before conv_done(op) can mark the bucket ready
                     call("channel_sum", dt, dy, M, op.cout, grad_of(op.conv.bias), acc, st)
-                if defer and op.needs_dgrad:
-                    bnr = (ctypes.addressof(op.bnr_desc) if op.bnr_desc is not None and self.bwd_conv_bn_reduce
-                           else None)
-                    call("conv2d_dgrad_ex", dt, dy, op.wt, dres, dmask, dx, B, op.H, op.W, op.cin_pad, op.cout, op.k,
-                         op.k, op.stride, op.pad, op.Ho, op.Wo, bnr, st)
-                    ws_j = self._wgrad_ws(op)
-                    batch.append((_WgradJob(op.src.t.data_ptr(), dy.data_ptr(), grad_of(op.conv.weight).data_ptr(),
-                                            ws_j.data_ptr(), ws_j.numel() * 4, B, op.H, op.W, op.cin_pad, op.cin,
-                                            op.cout, op.k, op.k, op.stride, op.pad, op.Ho, op.Wo, acc), op))
-                    if len(batch) == WGRAD_BATCH_MAX:
-                        flush_batch()
-                    continue
-                flush_batch()   # (the convs without a data gradient: the stem)
                 # data + weight gradient: one fused launch on the bf16 fast path
                 ws = ws_pp[slot]
                 dw = grad_of(op.conv.weight)
@@ -674,7 +635,6 @@ class TrunkEngine:
                 s = op.src
                 call("maxpool_bwd", dt, op.out.g, op.argmax, s.g, B, s.H, s.W, s.C, op.k, op.s, op.p, op.out.H,
                      op.out.W, st)
-        flush_batch()
         if pending is not None:
             call("wgrad_reduce", ctypes.addressof(pending), st)
             conv_done(pending_op)
@@ -706,21 +666,6 @@ class TrunkEngine:
     # training backward: a BN + ReLU whose output gradient one data-gradient launch
     # completes gets its reduce pass from that launch's epilogue (attribute for the tests)
     bwd_conv_bn_reduce = True
-    # training backward (bf16): weight gradients deferred into batched launches
-    # (pose6d_conv2d_wgrad_batch) instead of riding in each conv's fused launch
-    # (bit-identical; attribute for the tests / A/B)
-    defer_wgrad = False
-
-    def _wgrad_ws(self, op):
-        """This conv's own slab workspace for the batched weight gradient (the batch keeps
-        several convs' slabs alive at once)."""
-        ws = getattr(op, "ws_batch", None)
-        key = (self.B, self.dt)
-        if ws is None or getattr(op, "ws_batch_key", None) != key:
-            n = query("conv2d_wgrad_workspace", self.dt, self.B, op.Ho, op.Wo, op.cin_pad, op.cout, op.k, op.k)
-            op.ws_batch = ws = torch.empty(max(n // 4, 1), device=self.device, dtype=torch.float32)
-            op.ws_batch_key = key
-        return ws
 
     def set_dtype(self, dtype):
         self.dtype_req = dtype

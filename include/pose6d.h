@@ -398,27 +398,6 @@ int pose6d_conv2d_backward_chain_bn(int32_t dtype, const void *x, const void *dy
                                     int32_t Cin_real, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
                                     int32_t pad, int32_t Ho, int32_t Wo, const pose6d_wgrad_reduce_t *prev,
                                     int32_t *deferred, const pose6d_bn_reduce_t *bn, void *stream);
-/* Deferred weight gradients (round 5).  pose6d_conv2d_dgrad_ex: the data gradient of
- * pose6d_conv2d_backward_chain[_masked|_bn] alone (the same plan and bits; dres_mask and
- * bn may be NULL).  pose6d_conv2d_wgrad_batch: the weight gradients of up to
- * POSE6D_WGRAD_BATCH_MAX convs in ONE launch (each job: x, dy, its own slab workspace of
- * pose6d_conv2d_wgrad_workspace bytes, dw), then their slab reduces in one more launch
- * -- every dw bit-identical to pose6d_conv2d_wgrad of the same job.  bf16 only (the
- * LDS-DMA plans; a job whose plan is register-staged runs on its own). */
-#define POSE6D_WGRAD_BATCH_MAX 24
-typedef struct {
-  const void *x;        /* [N][H][W][Cin] */
-  const void *dy;       /* [N][Ho][Wo][Cout] */
-  float *dw;            /* OIHW fp32 [Cout][Cin_real][KH][KW] */
-  float *ws;            /* this job's slab workspace */
-  int64_t ws_bytes;
-  int32_t N, H, W, Cin, Cin_real, Cout, KH, KW, stride, pad, Ho, Wo, accumulate;
-} pose6d_wgrad_job_t;
-int pose6d_conv2d_dgrad_ex(int32_t dtype, const void *dy, const void *wt, const void *dres,
-                           const uint8_t *dres_mask, void *dx, int32_t N, int32_t H, int32_t W, int32_t Cin,
-                           int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad, int32_t Ho, int32_t Wo,
-                           const pose6d_bn_reduce_t *bn, void *stream);
-int pose6d_conv2d_wgrad_batch(int32_t dtype, const pose6d_wgrad_job_t *jobs, int32_t n, void *stream);
 /* (1 << 16) | (data-gradient mode << 4) | ring stages when pose6d_conv2d_backward
  * runs ONE fused conv_bwd_kernel<mode, stages, 3> launch (+ the reduce), else 0 */
 int pose6d_bwd_variant(int32_t dtype, int32_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t KH,
