@@ -88,6 +88,9 @@ struct Geom {
   int splits;
   int* sk_cnt;
   float* sk_part;
+  // fused backward (conv_bwd_kernel): each XCD walks its tiles as `win` interleaved
+  // streams (0 / 1 = in order); see conv_lds_body
+  int win;
 };
 
 // ---------------------------------------------------------------------------
@@ -852,7 +855,23 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   int bid = bid_in;
   {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int xs = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    int i = bid >> 3;
+    // fused backward: the data-gradient tiles of one XCD run as `win` interleaved
+    // streams over its M range -- the i-th dispatched workgroup takes step i / win of
+    // stream i % win -- so they read dY rows in step with the weight-gradient splits
+    // sharing the XCD (each streaming its own M range), not ahead of them all
+    if (g.win > 1) {
+      const int U = nsplit * (MODE == kDgradS2 && !g.s2one ? 4 : 1);   // ids that stay consecutive
+      const int L = (q + (xcd < r)) / U, iu = i / U;
+      if (iu < L) {
+        const int P = g.win < L ? g.win : L, Q = L / P, R = L - Q * P;
+        const int s = iu / P, j = iu - s * P;
+        i = (j < R ? j * (Q + 1) : R * (Q + 1) + (j - R) * Q) + s;
+        i = i * U + (bid >> 3) % U;
+      }
+    }
+    bid = xs + i;
   }
   // split-K: the splits of one tile are consecutive logical ids (one XCD, mostly)
   int split = 0;
@@ -1959,6 +1978,11 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
 #endif
   const int wfirst = order >= 0 ? order
                                 : (POSE6D_BWD_ORDER == 2 || (POSE6D_BWD_ORDER && WSTEP * p6::ceil_div(gw.mps, 64) >= nk));
+#ifndef POSE6D_BWD_WIN
+#define POSE6D_BWD_WIN 0   // build-time (A/B): data-gradient streams per XCD; 1 = one per weight-gradient split
+#endif
+  if (POSE6D_BWD_WIN == 1) gd.win = gw.splits >> 3;
+  else gd.win = POSE6D_BWD_WIN;
   const int grid = wfirst ? ((nw + 7) & ~7) + nd + rj.nblk : nd_pad + nw + rj.nblk;
   conv_bwd_kernel<DMODE, DS, WS, T><<<grid, kThreads, lds, s>>>(
       (const T*)dy, (const T*)wt, (const T*)dres, (T*)dx, gd, nd, nd_pad, wfirst, (const T*)x, ws, gw, rj);

@@ -265,7 +265,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_lds_kernel(const bf16* __
 // 32-pixel stages (32 KiB either way)
 template <int BT>
 constexpr int f32_ms() { return BT == 128 ? 32 : 64; }
-template <int S, bool PW, int BT>
+template <int S, bool PW, int BT, bool RT = false>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_lds_f32_kernel(const float* __restrict__ x,
                                                                       const float* __restrict__ dy,
                                                                       float* __restrict__ ws, WGeom g, ReduceJob rj) {
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_lds_f32_kernel(const floa
     run_reduce_job(smem, blockIdx.x - tiles * g.splits, rj);
     return;
   }
-  conv_wgrad_lds_body_f32<f32_ms<BT>(), S, PW, BT>(smem, blockIdx.x, x, dy, ws, g);
+  conv_wgrad_lds_body_f32<f32_ms<BT>(), S, PW, BT, RT>(smem, blockIdx.x, x, dy, ws, g);
 }
 
 template <int S, int BT>
@@ -283,6 +283,14 @@ int launch_fast_f32(const WGeom& g, const void* x, const void* dy, float* ws, hi
   int lds = S * WgF32<f32_ms<BT>(), BT>::STAGE;
   if (lds < acc_stage_bytes<BT, BT>()) lds = acc_stage_bytes<BT, BT>();
   const int grid = g.gm * g.gn * g.splits + rj.nblk;
+  if constexpr (BT == 64) {
+    if (g.kwp == p6::kRowTaps && g.SC == 4) {
+      conv_wgrad_lds_f32_kernel<S, false, 64, true><<<grid, kThreads, lds, s>>>((const float*)x, (const float*)dy, ws,
+                                                                               g, rj);
+      P6_LAUNCH_CHECK();
+      return POSE6D_OK;
+    }
+  }
   if (g.KH == 1 && g.KW == 1 && g.stride == 1 && g.pad == 0)
     conv_wgrad_lds_f32_kernel<S, true, BT><<<grid, kThreads, lds, s>>>((const float*)x, (const float*)dy, ws, g, rj);
   else
@@ -321,13 +329,17 @@ int tuned(const pose6d_tuning_t* t, int32_t pose6d_tuning_t::*f, int dflt) {
 #endif
 
 
+#ifndef POSE6D_WGRAD_TARGET_F32_RT
+#define POSE6D_WGRAD_TARGET_F32_RT 1024
+#endif
+
 #ifndef POSE6D_WGRAD_F32_KXK_BT
 #define POSE6D_WGRAD_F32_KXK_BT 128
 #endif
 
 // bf16 weight gradients take the LDS-DMA kernel (64x64 tiles, 3-slot ring) unless a
 // pose6d_tuning_t (tests / tools only) asks for the register-staged kernel or another ring
-// rowtap: the bf16 row-tap stem (wgrad_geom): SC is passed as 64 (its X image rows are
+// rowtap: the row-tap stems (wgrad_geom): SC is passed as 64 (its X image rows are
 // 64 K-elements by construction); it aims for ~4 workgroups per CU on a 2-slot ring --
 // its 4 K-tiles x 64 splits (one workgroup per CU, 98 64-pixel stages each) left each
 // workgroup waiting on its DMA: 56 -> 34 us graph-timed (profiles/r05w_stem_wgrad_sweep.txt)
@@ -362,6 +374,7 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
     min_rows = 256;
     step = f32_bt == 128 ? f32_ms<128>() : f32_ms<64>();
     max_bytes = 64ll << 20;
+    if (rowtap) target = POSE6D_WGRAD_TARGET_F32_RT;
   } else if (p.fast) {
     p.bm = 64;
     p.bn = 64;
@@ -491,7 +504,7 @@ extern "C" int64_t pose6d_conv2d_wgrad_workspace_tuned(int32_t dtype, int32_t N,
   }
   // (the stride / padding are not arguments: a 4-channel stem may take the row-tap plan,
   // whose slabs are wider -- report the larger of the two)
-  if (dtype == POSE6D_DT_BF16 && Cin == 4 && KH > 1 && KW <= p6::kRowTaps && Cout % 64 == 0) {
+  if (Cin == 4 && KH > 1 && KW <= p6::kRowTaps && Cout % 64 == 0) {
     const int Kpad = p6::ceil_div(KH * p6::kRowTaps * 4, 64) * 64;
     const Plan p = plan(dtype, N * Ho * Wo, Cout, Kpad, 64, tuning, true);
     const int64_t rt = (int64_t)p.splits * Cout * Kpad * 4;
@@ -515,9 +528,10 @@ WGeom wgrad_geom(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int 
   g.SH = H; g.SW = W; g.SC = Cin; g.log2SC = ilog2(Cin); g.RH = Ho; g.RW = Wo;
   g.KH = KH; g.KW = KW; g.stride = stride; g.pad = pad;
   g.kwp = KW;
-  // the bf16 4-channel stems: the LDS-DMA body on the row-tap X image (common.h), slabs in
-  // row-tap K order (64-column blocks = two kernel rows); the reduce maps them to OIHW
-  if (dtype == POSE6D_DT_BF16 && rowtap_geom(Cin, KH, KW, stride, pad) && Cout % 64 == 0 && (W & 1) == 0) {
+  // the 4-channel stems: the LDS-DMA body on the row-tap X image (common.h), slabs in
+  // row-tap K order (64-column blocks = two kernel rows); the reduce maps them to OIHW.
+  // (bf16 fetches two pixels per 16-byte chunk: even W; fp32 one pixel per chunk)
+  if (rowtap_geom(Cin, KH, KW, stride, pad) && Cout % 64 == 0 && (dtype == POSE6D_DT_F32 || (W & 1) == 0)) {
     const int Kpad = ceil_div(KH * kRowTaps * 4, 64) * 64;
     const Plan p = plan(dtype, g.M, Cout, Kpad, 64, tuning, true);   // (64: the LDS-DMA channel rule holds)
     if (p.fast) {

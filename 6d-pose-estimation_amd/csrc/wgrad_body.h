@@ -425,7 +425,9 @@ __device__ __forceinline__ void lds_wait_b32x4(float (&f)[4]) {
   asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]) : "n"(N));
 }
 
-template <int MS, int S, bool PW, int BT = 64>
+// RT: the fp32 row-tap stem (Cin = 4, 7x7 / stride 2): the 64-wide k tile is two kernel
+// rows of 8 taps x 4 channels (common.h rowtap_geom), one fetched chunk = one pixel
+template <int MS, int S, bool PW, int BT = 64, bool RT = false>
 __device__ __forceinline__ void conv_wgrad_lds_body_f32(char* smem, int bid, const float* __restrict__ x,
                                                         const float* __restrict__ dy, float* __restrict__ ws,
                                                         const p6::WGeom& g) {
@@ -453,6 +455,9 @@ __device__ __forceinline__ void conv_wgrad_lds_body_f32(char* smem, int bid, con
   // RPI - 1, the lane row RPI j + lane / CPR, chunk (lane % CPR) ^ (4 * odd row) of the row
   const int rsub = lane / C::CPR;
   const int ck = ((lane % C::CPR) ^ ((rsub & 1) << 2)) * 4;   // element offset of the fetched chunk
+  static_assert(!RT || (BT == 64 && !PW), "row-tap: 64-wide tiles");
+  // row-tap: kernel row and x offset of this lane's chunk (tap kw' = kw + 8 - KW)
+  const int rt_kr = (k0 + ck) >> 5, rt_dx = (((k0 + ck) & 31) >> 2) - (p6::kRowTaps - g.KW);
   int rm[PER], rn[PER], roy[PER], rox[PER];
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
@@ -476,6 +481,10 @@ __device__ __forceinline__ void conv_wgrad_lds_body_f32(char* smem, int bid, con
       const void* px = zp;
       if (PW) {
         if (ok) px = x + ((int64_t)rm[i] << g.log2SC) + ci0 + ck;
+      } else if (RT) {
+        const int yy = roy[i] * g.stride - g.pad + rt_kr, xx = rox[i] * g.stride - g.pad + rt_dx;
+        if (ok && rt_kr < g.KH && (unsigned)yy < (unsigned)g.SH && (unsigned)xx < (unsigned)g.SW)
+          px = x + ((((int64_t)rn[i] * g.SH + yy) * g.SW + xx) << 2);
       } else {
         const int yy = roy[i] * g.stride - g.pad + tkh, xx = rox[i] * g.stride - g.pad + tkw;
         if (ok && (unsigned)yy < (unsigned)g.SH && (unsigned)xx < (unsigned)g.SW)

@@ -709,10 +709,11 @@ def test_wgrad_fast_vs_register_staged(dtype):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [(2, 32, 32, 3, 64), (4, 224, 224, 3, 64), (2, 30, 26, 3, 128)])
-def test_stem_wgrad_rowtap(cfg):
-    """The bf16 4-channel 7x7 / stride-2 stem's weight gradient on the LDS-DMA body with
-    the row-tap X image (slabs in (kernel row, 8 taps, channel) order, mapped back to OIHW
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("cfg", [(2, 32, 32, 3, 64), (4, 224, 224, 3, 64), (2, 30, 26, 3, 128), (2, 29, 27, 3, 64)])
+def test_stem_wgrad_rowtap(cfg, dtype):
+    """The 4-channel 7x7 / stride-2 stem's weight gradient on the LDS-DMA body (bf16, and
+    the fp32 body: one pixel per 16-byte chunk, so odd widths too) with the row-tap X image (slabs in (kernel row, 8 taps, channel) order, mapped back to OIHW
     by the reduce): against the float64 torch op on the same bf16 operands, and against
     the register-staged kernel (Tuning(wgrad_base=1)); written and accumulated, standalone
     and in chain mode (pose6d_conv2d_backward_chain without a data gradient, carrying a
@@ -722,7 +723,7 @@ def test_stem_wgrad_rowtap(cfg):
     from pose6d.trunk import DTYPES, _WgradReduce
     N, H, W, Cin, Cout = cfg
     k, s, p, cp = 7, 2, 3, 4
-    dtype, dev = torch.bfloat16, "cuda"
+    dev = "cuda"
     dt = DTYPES[dtype]
     Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
     g = torch.Generator().manual_seed(N + H + Cout)
