@@ -88,9 +88,6 @@ struct Geom {
   int splits;
   int* sk_cnt;
   float* sk_part;
-  // fused backward (conv_bwd_kernel): each XCD walks its tiles as `win` interleaved
-  // streams (0 / 1 = in order); see conv_lds_body
-  int win;
 };
 
 // ---------------------------------------------------------------------------
@@ -855,23 +852,7 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
   int bid = bid_in;
   {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    const int xs = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-    int i = bid >> 3;
-    // fused backward: the data-gradient tiles of one XCD run as `win` interleaved
-    // streams over its M range -- the i-th dispatched workgroup takes step i / win of
-    // stream i % win -- so they read dY rows in step with the weight-gradient splits
-    // sharing the XCD (each streaming its own M range), not ahead of them all
-    if (g.win > 1) {
-      const int U = nsplit * (MODE == kDgradS2 && !g.s2one ? 4 : 1);   // ids that stay consecutive
-      const int L = (q + (xcd < r)) / U, iu = i / U;
-      if (iu < L) {
-        const int P = g.win < L ? g.win : L, Q = L / P, R = L - Q * P;
-        const int s = iu / P, j = iu - s * P;
-        i = (j < R ? j * (Q + 1) : R * (Q + 1) + (j - R) * Q) + s;
-        i = i * U + (bid >> 3) % U;
-      }
-    }
-    bid = xs + i;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
   // split-K: the splits of one tile are consecutive logical ids (one XCD, mostly)
   int split = 0;
@@ -1279,6 +1260,10 @@ __global__ __launch_bounds__(64 * NW) void conv_lds_kernel(const T* __restrict__
 // gradient workgroups they were the launch's tail.
 // T = float: the same launch for the reference-precision (fp32) step -- the fp32
 // LDS-DMA data gradient and the fp32 LDS-DMA weight gradient (wgrad_body.h).
+#ifndef POSE6D_BWD_F32_MS
+#define POSE6D_BWD_F32_MS 32   // build-time (A/B): pixels per fp32 weight-gradient stage in the fused launch
+#endif
+constexpr int kBwdF32MS = POSE6D_BWD_F32_MS;
 template <int DMODE, int DS, int WS, typename T = bf16>
 __global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ wt,
                                                             const T* __restrict__ dres, T* __restrict__ dx,
@@ -1299,7 +1284,7 @@ __global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const T* __restrict_
     if constexpr (sizeof(T) == 2)
       conv_wgrad_lds_body<64, 64, WS, DMODE == kGemm>(smem, b - w0, x, dy, ws, gw);
     else
-      conv_wgrad_lds_body_f32<64, WS, DMODE == kGemm>(smem, b - w0, x, dy, ws, gw);
+      conv_wgrad_lds_body_f32<kBwdF32MS, WS, DMODE == kGemm>(smem, b - w0, x, dy, ws, gw);
   } else if (b >= r0) {
     // the previous conv's weight-gradient slabs (another workspace), reduced here
     // instead of in a launch of their own
@@ -1962,7 +1947,7 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
   const int nk = fast_nk(DMODE, gd, LK<T>::KS);
   const int ring_d = (nk < DS ? (nk > 0 ? nk : 1) : DS) * 128 * 128;
   const int epi = 64 * (64 * (int)sizeof(T) + 16) + (gd.bnr_part ? bnr_lds(4, 64) : 0);
-  const int ring_w = sizeof(T) == 2 ? WS * 128 * 128 : WS * WgF32<64>::STAGE;
+  const int ring_w = sizeof(T) == 2 ? WS * 128 * 128 : WS * WgF32<kBwdF32MS>::STAGE;
   int lds = ring_d > epi ? ring_d : epi;
   lds = lds > ring_w ? lds : ring_w;
   // longest workgroups first: the weight gradient's K-steps per split against the
@@ -1978,11 +1963,6 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
 #endif
   const int wfirst = order >= 0 ? order
                                 : (POSE6D_BWD_ORDER == 2 || (POSE6D_BWD_ORDER && WSTEP * p6::ceil_div(gw.mps, 64) >= nk));
-#ifndef POSE6D_BWD_WIN
-#define POSE6D_BWD_WIN 0   // build-time (A/B): data-gradient streams per XCD; 1 = one per weight-gradient split
-#endif
-  if (POSE6D_BWD_WIN == 1) gd.win = gw.splits >> 3;
-  else gd.win = POSE6D_BWD_WIN;
   const int grid = wfirst ? ((nw + 7) & ~7) + nd + rj.nblk : nd_pad + nw + rj.nblk;
   conv_bwd_kernel<DMODE, DS, WS, T><<<grid, kThreads, lds, s>>>(
       (const T*)dy, (const T*)wt, (const T*)dres, (T*)dx, gd, nd, nd_pad, wfirst, (const T*)x, ws, gw, rj);
@@ -1990,14 +1970,21 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
   return POSE6D_OK;
 }
 
+// data-gradient ring depth of the fused launch for a plan of `stages` slots: fp32 plans
+// of 4 run 3, so that with the 32-pixel weight-gradient stages (kBwdF32MS) the launch
+// fits 48 KiB of LDS and three workgroups per CU (its VGPR budget allows three) -- the
+// fp32 step 12.19 -> 11.94 ms against 4 slots and 64-pixel stages (64 KiB, two per CU;
+// profiles/r05f32r_bwd_ring_ab.txt)
+int fused_ds(int dtype, int stages) { return dtype == POSE6D_DT_F32 && stages > 2 ? 3 : stages; }
+
 template <int DMODE>
 int launch_bwd_mode(int dtype, int ds, const Geom& gd, const p6::WGeom& gw, const void* dy, const void* wt,
                     const void* dres, void* dx, const void* x, float* ws, const ReduceJob& rj, hipStream_t s,
                     int order) {
   if (dtype == POSE6D_DT_F32)
-    return ds == 2 ? launch_bwd<DMODE, 2, POSE6D_WGRAD_STAGES_F32, float>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order)
-                   : launch_bwd<DMODE, 4, POSE6D_WGRAD_STAGES_F32, float>(gd, gw, dy, wt, dres, dx, x, ws, rj, s,
-                                                                           order);
+    return fused_ds(dtype, ds) == 2
+               ? launch_bwd<DMODE, 2, POSE6D_WGRAD_STAGES_F32, float>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order)
+               : launch_bwd<DMODE, 3, POSE6D_WGRAD_STAGES_F32, float>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order);
   return ds == 2 ? launch_bwd<DMODE, 2, POSE6D_WGRAD_STAGES>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order)
                  : launch_bwd<DMODE, 4, POSE6D_WGRAD_STAGES>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order);
 }
@@ -2217,7 +2204,7 @@ extern "C" int pose6d_bwd_variant(int32_t dtype, int32_t N, int32_t H, int32_t W
   const Plan pd = choose(dtype, mode, gd0, true);
   p6::WgradPlan pw;
   p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
-  return bwd_fused(dtype, pd, pw, nullptr) ? (1 << 16) | (pd.mode << 4) | pd.stages : 0;
+  return bwd_fused(dtype, pd, pw, nullptr) ? (1 << 16) | (pd.mode << 4) | fused_ds(dtype, pd.stages) : 0;
 }
 
 namespace {

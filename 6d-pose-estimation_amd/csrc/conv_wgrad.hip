@@ -329,10 +329,6 @@ int tuned(const pose6d_tuning_t* t, int32_t pose6d_tuning_t::*f, int dflt) {
 #endif
 
 
-#ifndef POSE6D_WGRAD_TARGET_F32_RT
-#define POSE6D_WGRAD_TARGET_F32_RT 1024
-#endif
-
 #ifndef POSE6D_WGRAD_F32_KXK_BT
 #define POSE6D_WGRAD_F32_KXK_BT 128
 #endif
@@ -342,7 +338,9 @@ int tuned(const pose6d_tuning_t* t, int32_t pose6d_tuning_t::*f, int dflt) {
 // rowtap: the row-tap stems (wgrad_geom): SC is passed as 64 (its X image rows are
 // 64 K-elements by construction); it aims for ~4 workgroups per CU on a 2-slot ring --
 // its 4 K-tiles x 64 splits (one workgroup per CU, 98 64-pixel stages each) left each
-// workgroup waiting on its DMA: 56 -> 34 us graph-timed (profiles/r05w_stem_wgrad_sweep.txt)
+// workgroup waiting on its DMA: 56 -> 34 us graph-timed (profiles/r05w_stem_wgrad_sweep.txt).
+// The fp32 row-tap stem keeps the fp32 default (512 -> 128 splits of its 4 tiles: 147 us
+// against 156 at 256 splits and 160 register-staged, profiles/r05w32_f32_stem_wgrad.txt)
 Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* tn = nullptr, bool rowtap = false) {
   Plan p{};
   // wgrad_base: 0 = default, 1 = register-staged; fp32 only: 2 = LDS-DMA 64x64 tiles,
@@ -374,7 +372,6 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
     min_rows = 256;
     step = f32_bt == 128 ? f32_ms<128>() : f32_ms<64>();
     max_bytes = 64ll << 20;
-    if (rowtap) target = POSE6D_WGRAD_TARGET_F32_RT;
   } else if (p.fast) {
     p.bm = 64;
     p.bn = 64;
