@@ -263,11 +263,8 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_lds_kernel(const bf16* __
 // workgroups run a carried slab reduce of the previous conv (`rj`), as the
 // register-staged kernel does.  64x64 tiles take 64-pixel stages, 128x128 tiles
 // 32-pixel stages (32 KiB either way)
-#ifndef POSE6D_WGRAD_F32_MS128
-#define POSE6D_WGRAD_F32_MS128 32   // build-time (A/B): pixels per stage of the 128x128 fp32 body
-#endif
 template <int BT>
-constexpr int f32_ms() { return BT == 128 ? POSE6D_WGRAD_F32_MS128 : 64; }
+constexpr int f32_ms() { return BT == 128 ? 32 : 64; }
 template <int S, bool PW, int BT, bool RT = false>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_lds_f32_kernel(const float* __restrict__ x,
                                                                       const float* __restrict__ dy,
@@ -284,7 +281,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_lds_f32_kernel(const floa
 template <int S, int BT>
 int launch_fast_f32(const WGeom& g, const void* x, const void* dy, float* ws, hipStream_t s, const ReduceJob& rj) {
   int lds = S * WgF32<f32_ms<BT>(), BT>::STAGE;
-  if (lds < acc_stage_bytes<BT, BT, (BT == 128)>()) lds = acc_stage_bytes<BT, BT, (BT == 128)>();
+  if (lds < acc_stage_bytes<BT, BT>()) lds = acc_stage_bytes<BT, BT>();
   const int grid = g.gm * g.gn * g.splits + rj.nblk;
   if constexpr (BT == 64) {
     if (g.kwp == p6::kRowTaps && g.SC == 4) {

@@ -63,46 +63,35 @@ namespace {
 // the dword form made the weight-gradient slab epilogue store-issue bound.
 // Entered after a barrier that ends every read of `smem`; needs BM * (BN + 16) * 4
 // bytes of it.  CHECK: clip rows >= rows / cols >= cols (partial tiles).
-// HALVES: the tile goes through LDS one half (the wm = 0 waves' rows, then wm = 1's) at
-// a time -- half the LDS (the fp32 128x128 weight gradient: 74 -> 37 KiB, so its ring
-// sets the launch's LDS); the same values land in the same places
-template <int BM, int BN, bool HALVES = false>
-constexpr int acc_stage_bytes() { return (HALVES ? BM / 2 : BM) * (BN + 16) * 4; }
+template <int BM, int BN>
+constexpr int acc_stage_bytes() { return BM * (BN + 16) * 4; }
 
-template <int BM, int BN, bool CHECK, bool HALVES = false>
+template <int BM, int BN, bool CHECK>
 __device__ __forceinline__ void store_acc_tile(const f32x4 (&acc)[BM / 32][BN / 32], char* smem, float* dst,
                                                int64_t ld, int rows, int cols) {
   constexpr int TM = BM / 32, TN = BN / 32;
   constexpr int LDT = BN + 16;              // floats per LDS row: rows alternate 16-bank halves
-  constexpr int H = HALVES ? 2 : 1, HR = BM / H;   // passes, rows per pass
   float* t = reinterpret_cast<float*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int grp = lane >> 4, li = lane & 15;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        t[(wm * (BM / 2) + i * 16 + grp * 4 + r) * LDT + wn * (BN / 2) + j * 16 + li] = acc[i][j][r];
+  __syncthreads();
   constexpr int CPR = BN / 4;               // float4 per row
   constexpr int RPP = 256 / CPR;            // rows per pass
   const int c4 = tid % CPR, r0 = tid / CPR;
 #pragma unroll
-  for (int h = 0; h < H; ++h) {
-    if (h > 0) __syncthreads();   // the previous half's LDS reads are done
-    if (!HALVES || wm == h) {
-      const int rb = HALVES ? 0 : wm * (BM / 2);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            t[(rb + i * 16 + grp * 4 + r) * LDT + wn * (BN / 2) + j * 16 + li] = acc[i][j][r];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int pass = 0; pass < HR / RPP; ++pass) {
-      const int lrow = pass * RPP + r0, row = h * HR + lrow;
-      const float4 v = *reinterpret_cast<const float4*>(t + lrow * LDT + c4 * 4);
-      if (CHECK && (row >= rows || c4 * 4 >= cols)) continue;
-      *reinterpret_cast<float4*>(dst + (int64_t)row * ld + c4 * 4) = v;
-    }
+  for (int pass = 0; pass < BM / RPP; ++pass) {
+    const int row = pass * RPP + r0;
+    const float4 v = *reinterpret_cast<const float4*>(t + row * LDT + c4 * 4);
+    if (CHECK && (row >= rows || c4 * 4 >= cols)) continue;
+    *reinterpret_cast<float4*>(dst + (int64_t)row * ld + c4 * 4) = v;
   }
 }
 
@@ -581,7 +570,7 @@ __device__ __forceinline__ void conv_wgrad_lds_body_f32(char* smem, int bid, con
   }
   asm volatile("s_barrier" ::: "memory");
   float* slab = ws + (int64_t)split * g.Cout * g.Kpad;
-  store_acc_tile<BT, BT, false, (BT == 128)>(acc, smem, slab + (int64_t)co0 * g.Kpad + k0, g.Kpad, BT, BT);
+  store_acc_tile<BT, BT, false>(acc, smem, slab + (int64_t)co0 * g.Kpad + k0, g.Kpad, BT, BT);
 }
 
 // sum the split slabs (fixed order) into the OIHW fp32 gradient; k = (kh, kw, ci).
