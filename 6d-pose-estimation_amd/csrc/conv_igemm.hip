@@ -1975,7 +1975,13 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
 // fits 48 KiB of LDS and three workgroups per CU (its VGPR budget allows three) -- the
 // fp32 step 12.19 -> 11.94 ms against 4 slots and 64-pixel stages (64 KiB, two per CU;
 // profiles/r05f32r_bwd_ring_ab.txt)
-int fused_ds(int dtype, int stages) { return dtype == POSE6D_DT_F32 && stages > 2 ? 3 : stages; }
+#ifndef POSE6D_BWD_BF16_DS4
+#define POSE6D_BWD_BF16_DS4 4   // build-time (A/B): the bf16 fused data-gradient ring for 4-slot plans
+#endif
+int fused_ds(int dtype, int stages) {
+  if (stages <= 2) return stages;
+  return dtype == POSE6D_DT_F32 ? 3 : POSE6D_BWD_BF16_DS4;
+}
 
 template <int DMODE>
 int launch_bwd_mode(int dtype, int ds, const Geom& gd, const p6::WGeom& gw, const void* dy, const void* wt,
@@ -1986,7 +1992,8 @@ int launch_bwd_mode(int dtype, int ds, const Geom& gd, const p6::WGeom& gw, cons
                ? launch_bwd<DMODE, 2, POSE6D_WGRAD_STAGES_F32, float>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order)
                : launch_bwd<DMODE, 3, POSE6D_WGRAD_STAGES_F32, float>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order);
   return ds == 2 ? launch_bwd<DMODE, 2, POSE6D_WGRAD_STAGES>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order)
-                 : launch_bwd<DMODE, 4, POSE6D_WGRAD_STAGES>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order);
+                 : launch_bwd<DMODE, POSE6D_BWD_BF16_DS4, POSE6D_WGRAD_STAGES>(gd, gw, dy, wt, dres, dx, x, ws, rj, s,
+                                                                               order);
 }
 
 }  // namespace
