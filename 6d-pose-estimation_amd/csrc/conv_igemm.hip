@@ -827,6 +827,9 @@ template <typename T> struct LK { static constexpr int CH = 16 / (int)sizeof(T),
 #ifndef POSE6D_EPI_PRE
 #define POSE6D_EPI_PRE 1
 #endif
+#ifndef POSE6D_S2_ROTATE
+#define POSE6D_S2_ROTATE 0   // build-time (A/B): rotate the parity-class order per tile (kDgradS2)
+#endif
 template <typename T, int BM, int BN, int MODE, int S, bool ACT = false, int NW = 4, bool BNR = false,
           bool PRE = false>
 __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* __restrict__ src,
@@ -872,7 +875,15 @@ __device__ __forceinline__ void conv_lds_body(char* smem, int bid_in, const T* _
     if (g.s2one) {
       cls = g.s2one - 1;
     } else {
+#if POSE6D_S2_ROTATE
+      // the four classes of tile t are logical ids 4t .. 4t+3 (one XCD, one L2), in an
+      // order that rotates with t: the dispatcher deals an XCD's workgroups out to its
+      // shader engines in turn, so a fixed order would give each engine one class (the
+      // 4-tap class's engine doing 4/9 of the work; a 1x1's tap class on one engine)
+      cls = 3 - ((bid + (bid >> 2)) & 3);
+#else
       cls = 3 - (bid & 3);
+#endif
       bid >>= 2;
     }
     py = cls >> 1; px = cls & 1;
