@@ -828,7 +828,7 @@ template <typename T> struct LK { static constexpr int CH = 16 / (int)sizeof(T),
 #define POSE6D_EPI_PRE 1
 #endif
 #ifndef POSE6D_S2_ROTATE
-#define POSE6D_S2_ROTATE 0   // build-time (A/B): rotate the parity-class order per tile (kDgradS2)
+#define POSE6D_S2_ROTATE 1   // build-time (A/B): 0 = the fixed class order (profiles/r05rot_s2_class_order_ab.txt)
 #endif
 template <typename T, int BM, int BN, int MODE, int S, bool ACT = false, int NW = 4, bool BNR = false,
           bool PRE = false>
