@@ -1603,6 +1603,15 @@ Plan choose(int dtype, int mode, const Geom& g, bool fused = false, const pose6d
     dflt_tile = (g.Ncols >= 512 && wg4 >= 96) ? 4 : 5;
   }
   if (ovr && POSE6D_FWD_TILE >= 0) dflt_tile = POSE6D_FWD_TILE;
+  // fp32 KxK stride-2 data gradients (four parity classes of 1-4 taps): 64x64 tiles on a
+  // 4-slot ring -- graph-timed 56x56 128->128 114.6 -> 94.1, 28x28 256->256 97.1 -> 92.0,
+  // 14x14 512->512 165.0 -> 111.7 us (profiles/r05s2st_f32_s2_dgrad_plan.txt)
+#ifndef POSE6D_F32_S2_PLAN
+#define POSE6D_F32_S2_PLAN 1   // build-time (A/B): 0 = the generic tile / ring rules
+#endif
+  const bool f32s2 = POSE6D_F32_S2_PLAN && dtype == POSE6D_DT_F32 && p.mode == kDgradS2 && !fused &&
+                     (g.KH > 1 || g.KW > 1);
+  if (f32s2) dflt_tile = 3;
   p.tile = (fused || mode == kGemmDual) ? 3 : tune(tn, &pose6d_tuning_t::conv_tile, dflt_tile);
   if (p.tile == 2 || p.tile < 0 || p.tile > 5) p.tile = 3;   // no 64x128 instance on the fast path
   // two slots (32 KiB at 64x64) keep several workgroups per CU resident, which hides
@@ -1617,7 +1626,7 @@ Plan choose(int dtype, int mode, const Geom& g, bool fused = false, const pose6d
   // fp32 forward (MFMA-bound: 4 exact 16x16x4 MFMAs per 16-byte chunk): 3 slots for
   // 1x1 filters, 2 for the rest (tools/conv_bench.py --graph --dtype f32 sweep, round 2)
   if (dtype == POSE6D_DT_F32 && (p.mode == kGemm || p.mode == kFwd)) dflt = (g.KH == 1 && g.KW == 1) ? 3 : 2;
-  if (long1x1) dflt = 4;
+  if (long1x1 || f32s2) dflt = 4;
   if (ovr && POSE6D_FWD_STAGES > 0) dflt = POSE6D_FWD_STAGES;
   p.stages = tune(tn, &pose6d_tuning_t::conv_stages, dflt);
   if (p.stages < 2) p.stages = 2;
