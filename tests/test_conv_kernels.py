@@ -29,6 +29,23 @@ def _close(got, ref, rtol, what):
     assert not bool(bad.any()), f"{what}: max err {err.max().item():.3e} (scale {scale:.3e}), {int(bad.sum())} bad"
 
 
+def test_s2_class_order_rotation():
+    """The stride-2 data gradient's workgroup -> (tile, parity class) map (conv_igemm.hip,
+    POSE6D_S2_ROTATE): logical ids 4t .. 4t+3 are tile t's four classes (a permutation,
+    so every output pixel is written exactly once, as before), and the class at each
+    position mod 4 -- the shader engine a dispatch round-robin hands it to -- rotates
+    with t, so every position sees each class equally often."""
+    T = 200
+    bid = np.arange(4 * T)
+    cls = 3 - ((bid + (bid >> 2)) & 3)
+    tile = bid >> 2
+    for t in range(T):
+        assert sorted(cls[tile == t].tolist()) == [0, 1, 2, 3]
+    for pos in range(4):
+        counts = np.bincount(cls[bid % 4 == pos], minlength=4)
+        assert counts.min() == counts.max() == T // 4
+
+
 _SKWS = {}
 
 
