@@ -286,9 +286,13 @@ class RGBDGeometricTrainer:
         cs = torch.cuda.Stream(device=self.dev)
         cs.wait_stream(torch.cuda.current_stream())
 
+        # thread-local capture: the RCCL watchdog thread keeps querying the events of
+        # earlier all-reduces while these segments are captured; under the default
+        # (global) mode such a call from another thread is illegal during a capture and
+        # the watchdog aborts the process
         def begin():
             st["g"] = torch.cuda.CUDAGraph()
-            st["g"].capture_begin(pool=pool)
+            st["g"].capture_begin(pool=pool, capture_error_mode="thread_local")
 
         def cut(upto):
             # the last bucket (ending at the arena end) always goes out after the
@@ -314,7 +318,7 @@ class RGBDGeometricTrainer:
             st["g"].capture_end()
             segs.append((st["g"], (st["next"], len(ends))))
             opt = torch.cuda.CUDAGraph()
-            opt.capture_begin(pool=pool)
+            opt.capture_begin(pool=pool, capture_error_mode="thread_local")
             self._optimizer()
             opt.capture_end()
         torch.cuda.current_stream().wait_stream(cs)
