@@ -246,17 +246,23 @@ def main():
                    "global_batch": world * B, "per_gpu_batch": B, "crop": "224x224", "seq_len": None,
                    "parallelism": f"dp{world}", "loss": float(loss)},
     }
-    if rank == 0 and not args.no_kernel_profile:
+    # the roofline / fp32 / side / CPU measurements run at N=1 only: they capture graphs of
+    # their own, and under a live RCCL process group a global-mode capture races the
+    # watchdog thread's event queries (DESIGN: Multi-GPU); the scaling lines need none of them
+    solo = world == 1
+    if not solo:
+        result["side_measurements"] = "N=1 only (roofline, fp32_train, side_configs, cpu_baseline)"
+    if rank == 0 and solo and not args.no_kernel_profile:
         result.update(kernel_profile(tr, data, ms))
-    if rank == 0 and not args.no_fp32:
+    if rank == 0 and solo and not args.no_fp32:
         # the same step in the reference's fp32 arithmetic (this headline line is bf16,
         # BASELINE configs[2]: narrower than the reference's fp32 training)
         result["fp32_train"] = fp32_train(dev, args.steps, args.warmup, B)
-    if rank == 0 and not args.no_side:
+    if rank == 0 and solo and not args.no_side:
         result["side_configs"] = {"configs[1]": rgb_fp32_forward(dev), "dropin_fp32_train": dropin_fp32_train(dev),
                                   "configs[3]": add_eval_throughput(dev, cpu=not args.no_cpu_baseline),
                                   "frame_crops": crop_throughput(dev), "inference_b1": inference_latency(dev)}
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and solo and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline()
         except Exception as e:  # noqa: BLE001 - report, do not fail the bench line
