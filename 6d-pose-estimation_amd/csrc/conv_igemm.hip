@@ -1695,19 +1695,10 @@ int64_t splitk_need(const Plan& p) {
 int run_conv(int dtype, int mode, const Geom& g, const void* src, const void* w, const float* bias, const void* res,
              void* out, float* stats, hipStream_t s, const pose6d_tuning_t* tn = nullptr, bool fwd = false,
              void* sk_ws = nullptr, int64_t sk_bytes = 0) {
-  Plan p = choose(dtype, mode, g, false, tn, fwd);
-  const int64_t need = splitk_need(p);
-  if (need > 0) {
-    P6_CHECK_ARG(sk_ws != nullptr && sk_bytes >= need,
-                 "conv: this plan splits K over %d workgroups per tile (pose6d_conv_variant >> 16) and needs a split-K "
-                 "workspace of %lld bytes (pose6d_conv_splitk_workspace), got %lld",
-                 p.g.splits, (long long)need, (long long)(sk_ws ? sk_bytes : 0));
-    P6_CHECK_ARG(((uintptr_t)sk_ws & 255) == 0, "conv: the split-K workspace must be 256-byte aligned");
-    p.g.sk_cnt = (int*)sk_ws;
-    p.g.sk_part = (float*)((char*)sk_ws + kSkCntBytes);
-  }
-  // 3x3 stride-1 bf16 forwards without BatchNorm statistics (eval; conv_patch.h): the
-  // input patch staged once per 64-channel slice instead of once per filter tap
+  // 3x3 stride-1 bf16 forwards without BatchNorm statistics (eval; conv_patch.h: the
+  // input patch staged once per 64-channel slice instead of once per filter tap) are
+  // decided first -- the patch kernel never splits K, so it needs no split-K workspace
+  // even where the implicit-GEMM plan of the same geometry would
   {
     PatchPlan pp{};
     if (patch_eligible(dtype, mode, g, stats, tn, &pp)) {
@@ -1723,6 +1714,17 @@ int run_conv(int dtype, int mode, const Geom& g, const void* src, const void* w,
         default: return launch_patch<kPatchStages>(g, pp, N, src, w, bias, res, out, s);
       }
     }
+  }
+  Plan p = choose(dtype, mode, g, false, tn, fwd);
+  const int64_t need = splitk_need(p);
+  if (need > 0) {
+    P6_CHECK_ARG(sk_ws != nullptr && sk_bytes >= need,
+                 "conv: this plan splits K over %d workgroups per tile (pose6d_conv_variant >> 16) and needs a split-K "
+                 "workspace of %lld bytes (pose6d_conv_splitk_workspace), got %lld",
+                 p.g.splits, (long long)need, (long long)(sk_ws ? sk_bytes : 0));
+    P6_CHECK_ARG(((uintptr_t)sk_ws & 255) == 0, "conv: the split-K workspace must be 256-byte aligned");
+    p.g.sk_cnt = (int*)sk_ws;
+    p.g.sk_part = (float*)((char*)sk_ws + kSkCntBytes);
   }
   if (p.fast) return dispatch_fast(dtype, p.mode, p.g, p.tile, p.stages, src, w, bias, res, out, stats, s);
   return dtype == POSE6D_DT_BF16 ? dispatch<bf16>(mode, g, p.tile, src, w, bias, res, out, stats, s)

@@ -378,6 +378,10 @@ static int packed_jobs(const void* descs, int32_t n_desc, const float* param, in
     const int kwp = d[k].KWp > 0 ? d[k].KWp : d[k].KW;
     P6_CHECK_ARG(kwp >= d[k].KW && d[k].Kpad >= d[k].KH * kwp * d[k].Ip && d[k].Ip >= d[k].I && (d[k].Kpad & 3) == 0,
                  "pose6d_adamw_packed_jobs: conv %d: bad packed geometry", k);
+    // a tile holds one channel's taps at least: KH * KW must fit the LDS tile's columns
+    P6_CHECK_ARG(d[k].KH * d[k].KW <= kTileCols,
+                 "pose6d_adamw_packed_jobs: conv %d: %d x %d filter taps exceed the %d-column packing tile", k,
+                 d[k].KH, d[k].KW, kTileCols);
     reg.push_back({off, k});
   }
   std::sort(reg.begin(), reg.end());

@@ -64,3 +64,14 @@ class EngineModel(nn.Module):
 
     def engines(self):
         return dict(self._p6_engines)
+
+    def sync_weights(self):
+        """Re-pack every trunk engine's compute-dtype conv weights from the fp32
+        masters now.  Forwards re-pack by themselves after writes torch's version
+        counters record (load_state_dict, optimizer steps, in-place ops on a
+        Parameter); a write through `p.data` (a `.data` alias has a version counter
+        of its own) or a raw pointer is invisible to them and needs this call."""
+        for eng in self._p6_engines.values():
+            if isinstance(eng, TrunkEngine) and getattr(eng, "_shape", None) is not None:
+                eng.pack_weights(force=True)
+        return self

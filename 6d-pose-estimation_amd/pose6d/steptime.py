@@ -256,7 +256,9 @@ class StepTimer:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph(keep_graph=True)
-        with torch.cuda.graph(self.graph, stream=s):
+        # thread-local capture: under a live RCCL group the watchdog thread queries the
+        # events of in-flight collectives meanwhile, which a global-mode capture forbids
+        with torch.cuda.graph(self.graph, stream=s, capture_error_mode="thread_local"):
             log = _CallLog(torch.cuda.current_stream().cuda_stream)
             _lib.observers.append(log)
             try:

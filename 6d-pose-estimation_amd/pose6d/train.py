@@ -13,9 +13,13 @@ MI355X design:
     so replays stay exact;
   * the AdamW launch also writes the convs' packed compute-dtype weights
     (pose6d_adamw_step_packed): the next forward reads them with no packing pass
-    over the updated masters.  A write to the masters from outside the step
-    (restore, load_state_dict, ...) is seen through torch's version counters and
-    re-packed before the next step;
+    over the updated masters.  A write to the masters from outside the step that
+    goes through the arena or a Parameter (restore, load_state_dict, an in-place op
+    on a Parameter under no_grad) is seen through torch's version counters and
+    re-packed before the next step.  A write through `p.data` (e.g.
+    `p.data.copy_(w)`) is NOT seen -- `.data` is an alias with a version counter
+    of its own -- so such a caller must call sync_weights() afterwards (as a
+    torch user must re-run anything cached from the old values);
   * data parallel: one process per GPU, batch shards, gradient all-reduce over
     RCCL (torch.distributed 'nccl'); bucketed all-reduces are issued on a comm
     stream as soon as each bucket's gradients exist, overlapping the rest of the
@@ -148,13 +152,18 @@ class RGBDGeometricTrainer:
         self.n_jobs = n
 
     def _weights_key(self):
-        # writes through the arena (restore) bump flat's counter; writes through a
-        # Parameter (load_state_dict, p.data.copy_) bump that Parameter's own
+        # writes through the arena (restore) bump flat's counter; in-place writes to a
+        # Parameter (load_state_dict, `with torch.no_grad(): p.copy_(w)`) bump that
+        # Parameter's own.  `p.data.copy_(w)` bumps neither (a `.data` alias carries a
+        # fresh version counter): sync_weights() is the documented call after it
         return (self.arena.flat._version,) + tuple(op.conv.weight._version for op in self.trunk.convs)
 
     def sync_weights(self):
         """Re-pack the conv weights from the fp32 masters (one launch).  step() calls
-        it when the masters were written from outside the step."""
+        it itself when a version counter shows the masters were written from outside
+        the step; after a write the counters cannot see -- through `p.data` or a raw
+        pointer (ctypes, another library) -- the caller must call it before the next
+        step() or eval forward."""
         self.trunk.pack_weights(force=True)
         self._packed_key = self._weights_key()
 
@@ -268,7 +277,7 @@ class RGBDGeometricTrainer:
         torch.cuda.synchronize()
         if not self._ddp:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self.step_body(data)
             self.graphs = [g]
         else:

@@ -372,7 +372,8 @@ class TrunkEngine:
         B, C, H, W = x.shape
         if C != self.in_channels:
             raise Pose6dError(f"trunk expects {self.in_channels} input channels, got {C}")
-        self.prepare(B, H, W, self.dtype_req, x.device)
+        padw = self._stem_pad_cols(W, self.dtype_req)
+        self.prepare(B, H, W + padw, self.dtype_req, x.device)
         if pack:
             self.pack_weights()
         st = stream()
@@ -380,8 +381,12 @@ class TrunkEngine:
         xf = x.detach()
         if xf.dtype != torch.float32:
             xf = xf.float()
+        if padw:
+            # odd-width bf16 input to a row-tap stem: one zero column on the right (exact:
+            # see _stem_pad_cols); torch does the copy, the trunk runs on the even width
+            xf = torch.nn.functional.pad(xf, (0, padw))
         xf = xf.contiguous()
-        call("nchw_to_nhwc", dt, xf, self.input.t, B, C, H, W, self.input.C, st)
+        call("nchw_to_nhwc", dt, xf, self.input.t, B, C, H, W + padw, self.input.C, st)
         # eval: the BN (running statistics) is known before the conv runs, so the conv's
         # epilogue applies BN (+ residual) + ReLU and stores the activation directly
         fold = not training and self.eval_fuse
@@ -470,6 +475,25 @@ class TrunkEngine:
         self._saved_gen = self.generation if training else -1
         self._eval_gen = -1 if training else self.generation
         return self.feat
+
+    def _stem_pad_cols(self, W, dtype):
+        """1 if the first conv is a bf16 row-tap stem (4-channel 7x7 / stride 2,
+        pose6d_conv_pack_geom) and W is odd, else 0.  The bf16 row-tap kernels read two
+        pixels per 16-byte chunk from even pixel offsets, so they need an even row pitch
+        (pose6d_conv2d_fwd refuses odd W); a zero column appended on the right gives the
+        same output width -- floor((W + 1 + 2p - k) / s) == floor((W + 2p - k) / s) for
+        the stride-2 stems at odd W -- and every window that reaches it reads zero
+        padding there already, so the result is the odd-width conv's exactly (the stem
+        has no data gradient; its weight gradient sees a zero column)."""
+        if dtype != torch.bfloat16 or W % 2 == 0:
+            return 0
+        c = self.seq[0]
+        k, s, p = c.kernel_size[1], c.stride[1], c.padding[1]
+        cin_pad = 4 if self.in_channels < 8 else self.in_channels
+        if pack_geom(dtype, cin_pad, k, s, p)[0] == k:
+            return 0   # not a row-tap stem: any width works
+        assert (W + 1 + 2 * p - k) // s == (W + 2 * p - k) // s, "row-tap stem: padding would change Wo"
+        return 1
 
     def _dual_pairs(self):
         """Eval: each Bottleneck with a downsample branch gets its output from ONE launch

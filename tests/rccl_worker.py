@@ -5,6 +5,8 @@ buckets, the comm stream, async all-reduce handles around the segmented-graph re
 (RGBDGeometricTrainer(force_buckets=True)) -- at bs32 bf16 (BASELINE configs[4] per rank).
 An all-reduce over one rank returns its input, so eager and replayed steps must equal
 the plain world-1 step bit for bit (parameters, AdamW moments, BN running statistics).
+Then the in-step kernel timer bench.py's roofline uses (pose6d.steptime) captures and
+replays the step once under the same live group.
 argv: OUT"""
 import os
 import sys
@@ -63,8 +65,20 @@ def main():
     torch.cuda.synchronize()
     graph_same = torch.equal(state(trg), want)
     n_segs = len(trg.graphs) - 1
+    # bench.py's in-step roofline capture under the live group (thread-local capture
+    # mode): an all-reduce is left in flight so the RCCL watchdog thread is polling its
+    # event while the step is captured and instrumented
+    from pose6d import steptime
+    pending = torch.ones(1 << 20, device=dev)
+    work = dist.all_reduce(pending, async_op=True)
+    timer = steptime.StepTimer(lambda: ref.step_body(data), dev)
+    recs = timer.run(2)
+    timer.close()
+    work.wait()
+    torch.cuda.synchronize()
+    timed = sum(1 for r in recs if r["us"] > 0)
     with open(out, "w") as f:
-        f.write(f"{int(eager_same)} {int(graph_same)} {n_buckets} {n_segs} {dist.get_backend()}\n")
+        f.write(f"{int(eager_same)} {int(graph_same)} {n_buckets} {n_segs} {dist.get_backend()} {timed}\n")
     dist.destroy_process_group()
 
 

@@ -70,6 +70,12 @@ def test_packed_jobs_reject_bad_tables():
     assert query("adamw_packed_jobs", rec.ctypes.data, 2, base, 8192, None, 0) < 0   # past the end
     rec[1] = (base + 4 * 4097, 0x1000, 0, 64, 64, 64, 1, 1, 64, 1, 0, 0)
     assert query("adamw_packed_jobs", rec.ctypes.data, 2, base, 1 << 16, None, 0) < 0   # misaligned
+    # a filter whose taps exceed the kernel's 128-column LDS tile (13 x 13 = 169) is refused
+    one = np.zeros(1, _DESC)
+    one[0] = (base, 0x1000, 0, 8, 8, 8, 13, 13, 13 * 13 * 8, 13, 0, 0)
+    assert query("adamw_packed_jobs", one.ctypes.data, 1, base, 1 << 16, None, 0) < 0
+    one[0] = (base, 0x1000, 0, 8, 8, 8, 11, 11, 11 * 11 * 8, 11, 0, 0)   # 121 taps fit
+    assert query("adamw_packed_jobs", one.ctypes.data, 1, base, 1 << 16, None, 0) > 0
 
 
 def _pair(dtype, B=4):
@@ -122,3 +128,21 @@ def test_packed_adamw_bit_identical_to_pack_pass(dtype):
         t.step()
     torch.cuda.synchronize()
     _assert_same(trs[0], trs[1], "after load_state_dict")
+    # an in-place write to a Parameter under no_grad bumps its version counter: seen
+    torch.manual_seed(2)
+    w = torch.randn_like(trs[0].trunk.convs[5].conv.weight)
+    for t in trs:
+        with torch.no_grad():
+            t.trunk.convs[5].conv.weight.copy_(w)
+        t.step()
+    torch.cuda.synchronize()
+    _assert_same(trs[0], trs[1], "after an in-place Parameter write")
+    # a write through `.data` is invisible to the version counters (a `.data` alias has
+    # its own): the documented contract is an explicit sync_weights() before the next step
+    w = torch.randn_like(trs[0].trunk.convs[7].conv.weight)
+    for t in trs:
+        t.trunk.convs[7].conv.weight.data.copy_(w)
+        t.sync_weights()
+        t.step()
+    torch.cuda.synchronize()
+    _assert_same(trs[0], trs[1], "after p.data.copy_ + sync_weights()")

@@ -10,7 +10,8 @@
     against torch's clip_grad_norm_ + AdamW on the same gradients;
   - the benchmarked bf16 trainer op by op ("teacher forced"): every conv forward,
     BN statistics + apply, pooling, the fp32 head + loss, every BN backward, every
-    conv weight gradient and the single-consumer data gradients are checked
+    conv weight gradient, every data gradient (the 16 residual junctions as the sum
+    of their consumers' contributions) and the stem's max-pool backward are checked
     against torch-CPU fp32 ops applied to the SAME bf16 operands the step used.
     End-to-end fp32-vs-bf16 comparison is meaningless for a random-init ResNet50:
     on the oracle itself, rounding only the input image to bf16 (0.4 %) moves
@@ -173,6 +174,32 @@ class _Tol:
         assert not bad, bad
 
 
+def _check_pool_bwd(T, pool):
+    """The stem's max-pool backward: the pooled gradient routed to the input pixel the
+    forward's argmax names (window index kh * k + kw; the first maximum), summed over the
+    windows that share a pixel.  The argmax is checked too: the pixel it names must hold
+    the window's maximum of the reference pool input (within the stored tolerance)."""
+    a, c = pool.act, pool.act.cop
+    B, Ho, Wo, C = pool.argmax.shape
+    H, W, k, s, p = pool.src.H, pool.src.W, pool.k, pool.s, pool.p
+    idx = pool.argmax.long().cpu()
+    oy = torch.arange(Ho).view(1, Ho, 1, 1)
+    ox = torch.arange(Wo).view(1, 1, Wo, 1)
+    iy, ix = oy * s - p + idx // k, ox * s - p + idx % k
+    assert bool(((iy >= 0) & (iy < H) & (ix >= 0) & (ix < W)).all()), "argmax names a padding position"
+    n = torch.arange(B).view(B, 1, 1, 1)
+    ch = torch.arange(C).view(1, 1, 1, C)
+    flat = (((n * H + iy) * W + ix) * C + ch).flatten()
+    dy = pool.out.g.detach().float().cpu().flatten()
+    ref = torch.zeros(B * H * W * C).index_add_(0, flat, dy).view(B, H, W, C).permute(0, 3, 1, 2)
+    T.stored(f"pool bwd:{a.out.name}", _nchw(a.out.g), ref)
+    # the pool input the kernel saw: bf16(max(y * scale + shift, 0))
+    y = c.out.t.detach().double().cpu()
+    z = (y * c.scale.cpu().double() + c.shift.cpu().double()).clamp_min(0).float().bfloat16().float()
+    picked = z.flatten()[flat].view(B, Ho, Wo, C).permute(0, 3, 1, 2)
+    T.stored(f"pool argmax:{pool.out.name}", picked, _nchw(pool.out.t))
+
+
 @pytest.mark.gpu
 def test_configs2_trainer_bs32_bf16_teacher_forced():
     from pose6d.trunk import _ActOp, _ConvOp, _PoolOp
@@ -246,22 +273,24 @@ def test_configs2_trainer_bs32_bf16_teacher_forced():
         else:
             T.sums(f"head:grad {k}", grad(named[k]), v.grad, 1e-4)
 
-    # backward: BN (from our dout), conv weight gradients and single-consumer data gradients
-    consumers = {}
-    for op in trunk.ops:
-        for a in ("src", "res_act"):
-            t = getattr(op, a, None)
-            if t is not None:
-                consumers[id(t)] = consumers.get(id(t), 0) + 1
+    # backward: BN (from our dout), conv weight gradients, and every data gradient where
+    # the contributions meet -- a conv input's gradient is the sum over its consumers:
+    # each reading conv's data gradient, plus, for a block input, the identity branch's
+    # share dout * mask of the block output (added in the conv1 data-gradient epilogue),
+    # or the downsample conv's data gradient (added in place after conv1's)
     for op in trunk.ops:
         if isinstance(op, _ActOp):
             c = op.cop
-            dout = _nchw(op.out.g) if not op.pooled else None
-            if op.pooled:
-                continue   # stem: its dout is the max-pool gradient (checked below through dW of the stem)
+            dout = _nchw(op.out.g)
             y = _nchw(c.out.t)
-            # the ReLU mask the kernels use: stored output > 0
-            mask = (_nchw(op.out.t) > 0).float() if op.relu else torch.ones_like(y)
+            if op.pooled:
+                # the stem: its BN + ReLU lives in the max pool; the backward recomputes the
+                # ReLU sign from y (exact in fp64: fmaf rounding keeps the sign)
+                pre = y.double() * c.scale.cpu().double().view(1, -1, 1, 1) + c.shift.cpu().double().view(1, -1, 1, 1)
+                mask = (pre > 0).float()
+            else:
+                # the ReLU mask the kernels use: stored output > 0
+                mask = (_nchw(op.out.t) > 0).float() if op.relu else torch.ones_like(y)
             dz = dout * mask
             xh = (y - c.mean.cpu().view(1, -1, 1, 1)) * c.inv.cpu().view(1, -1, 1, 1)
             M = y.numel() // y.shape[1]
@@ -277,9 +306,32 @@ def test_configs2_trainer_bs32_bf16_teacher_forced():
             dy = _nchw(op.out.g)
             dW = torch.nn.grad.conv2d_weight(x, Wb.shape, dy, op.stride, op.pad)
             T.sums(f"conv wgrad:{op.out.name}", grad(op.conv.weight), dW)
-            if op.needs_dgrad and consumers.get(id(op.src), 0) == 1 and op.src is not trunk.input:
-                dx = torch.nn.grad.conv2d_input(x.shape, Wb, dy, op.stride, op.pad)
-                T.stored(f"conv dgrad:{op.out.name}", _nchw(op.src.g), dx)
+        elif isinstance(op, _PoolOp) and op.act is not None:
+            _check_pool_bwd(T, op)
+    contrib = {}
+    for op in trunk.ops:
+        if isinstance(op, _ConvOp) and op.needs_dgrad:
+            x = _nchw(op.src.t)[:, :op.cin]
+            Wb = w0(op.conv.weight).bfloat16().float()
+            dx = torch.nn.grad.conv2d_input(x.shape, Wb, _nchw(op.out.g), op.stride, op.pad)
+            contrib.setdefault(id(op.src), (op.src, []))[1].append(("conv", dx))
+        elif isinstance(op, _ActOp) and op.res_act is not None:
+            mask = (_nchw(op.out.t) > 0).float() if op.relu else 1.0
+            contrib.setdefault(id(op.res_act), (op.res_act, []))[1].append(("res", _nchw(op.out.g) * mask))
+    junctions = 0
+    for src, parts in contrib.values():
+        kind = "conv dgrad" if len(parts) == 1 else "junction dgrad"
+        junctions += len(parts) > 1
+        extra = None
+        if len(parts) > 1:
+            # the data-gradient epilogue rounds its accumulator to bf16 (the tile is staged
+            # through LDS as T) before it adds the waiting contribution -- the identity
+            # branch's dout * mask, or conv1's stored data gradient that the downsample
+            # conv's epilogue accumulates in place -- exactly as a separate add of two
+            # bf16 tensors would: each conv term carries one bf16 rounding of its own
+            extra = 2.0 ** -7 * sum(t.abs() for k, t in parts if k == "conv")
+        T.stored(f"{kind}:{src.name}", _nchw(src.g), sum(t for _, t in parts), extra)
+    assert junctions == 16, junctions   # every Bottleneck's input: 4 downsampling + 12 identity blocks
     T.check()
     _check_adamw(tr, before)
 

@@ -12,6 +12,16 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _report(r):
+    """A failed subprocess's output for the assertion message: the head of stderr (a
+    watchdog or collective error is printed first, then buried under the launcher's
+    per-rank tracebacks), every line naming an error, and the tails."""
+    err = r.stderr.splitlines()
+    flagged = [ln for ln in err if any(k in ln for k in ("Error", "error", "Watchdog", "watchdog", "abort", "Abort"))]
+    return ("--- stderr head ---\n" + "\n".join(err[:60]) + "\n--- error lines ---\n" + "\n".join(flagged[:80])
+            + "\n--- stdout tail ---\n" + r.stdout[-3000:] + "\n--- stderr tail ---\n" + r.stderr[-3000:])
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,batch,bucket_mb", [(2, 4, 2.0), (3, 4, 2.0), (2, 32, 25.0)],
                          ids=["w2-b4", "w3-b4", "w2-b32-configs4"])
@@ -24,7 +34,7 @@ def test_ddp_bucketed_step_matches_mean_gradient_update(world, batch, bucket_mb)
            "--master-addr", "127.0.0.1", "--master-port", str(29631 + world + batch),
            os.path.join(REPO, "tests", "ddp_worker.py"), out, str(batch), str(bucket_mb)]
     r = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _report(r)
     for rank in range(world):
         f = open(f"{out}.{rank}").read().split()
         same, diff, graph_same, run_eager, run_graph, agree, nb, nsegs, distinct = f
@@ -48,7 +58,7 @@ def test_bench_world2_json_line():
            "--master-addr", "127.0.0.1", "--master-port", "29671", os.path.join(REPO, "bench.py"), "--gpus", "2",
            "--steps", "3", "--warmup", "1", "--no-side", "--no-fp32", "--no-cpu-baseline", "--no-kernel-profile"]
     r = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _report(r)
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-3000:]
     res = json.loads(lines[0])
@@ -63,16 +73,21 @@ def test_rccl_world1_bucketed_step():
     for N > 1): one rank under torch.distributed.run, the trainer forced onto the
     bucketed path (25 MB buckets, comm stream, async all-reduce handles around the
     segmented-graph replay).  A one-rank all-reduce returns its input, so two eager and
-    two replayed steps equal the plain one-GPU steps bit for bit.  Scaling over xGMI
-    stays unmeasured here (one GPU per box)."""
+    two replayed steps equal the plain one-GPU steps bit for bit.  Then bench.py's
+    in-step roofline capture (pose6d.steptime) runs once under the same live group, with
+    an all-reduce in flight for the RCCL watchdog to poll.  Scaling over xGMI stays
+    unmeasured here (one GPU per box)."""
     out = os.path.join(tempfile.mkdtemp(), "rccl")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
            "--master-addr", "127.0.0.1", "--master-port", "29691", os.path.join(REPO, "tests", "rccl_worker.py"), out]
     r = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    eager_same, graph_same, nb, nsegs, backend = open(out).read().split()
+    assert r.returncode == 0, _report(r)
+    eager_same, graph_same, nb, nsegs, backend, timed = open(out).read().split()
     assert backend == "nccl"
+    # the in-step roofline capture (pose6d.steptime, thread-local capture mode) ran once
+    # under the live RCCL group with an all-reduce in flight: its kernel records came back
+    assert int(timed) > 100, f"steptime under RCCL recorded {timed} kernels"
     assert int(nb) >= 4 and int(nsegs) >= 3, "expected several 25 MB buckets and graph segments"
     assert eager_same == "1", "eager bucketed RCCL step != plain one-GPU step"
     assert graph_same == "1", "segmented-graph RCCL step != plain one-GPU step"

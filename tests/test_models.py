@@ -240,3 +240,46 @@ def test_train_step_parity_fp32(name):
             a, b = named[k].grad.double().cpu().flatten(), v.grad.double().flatten()
             cos = (a @ b / (a.norm() * b.norm() + 1e-300)).item()
             assert cos > 0.99 or b.norm() < 1e-12, f"grad {k}: cosine {cos:.4f}"
+
+
+@pytest.mark.gpu
+def test_bf16_trunk_odd_width_row_tap_stem():
+    """Odd input widths on the bf16 trunk: the bf16 row-tap stem kernels
+    need an even row pitch, so TrunkEngine appends one zero column (exact: same output
+    width, the column lies in the conv's zero padding).  Checked against torch-CPU fp32
+    ops on the same bf16 operands: the stem forward (stored tensor within one bf16 ulp
+    + 1e-3 of its RMS) and the stem weight gradient (1e-3 Frobenius), plus a z-CNN
+    (PoseNetRGBGeometric) forward on the same odd width."""
+    import torch.nn.functional as F
+    from models.pose_net_rgb_geometric import PoseNetRGBGeometric
+    from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
+    from pose6d.trunk import TrunkEngine
+    warnings.simplefilter("ignore")
+    torch.manual_seed(0)
+    m = PoseNetRGBDGeometric(pretrained=False).cuda().train()
+    eng = TrunkEngine(m.backbone, 3)
+    eng.set_dtype(torch.bfloat16)
+    x = torch.randn(2, 3, 64, 63, generator=torch.Generator().manual_seed(3))
+    feat = eng.forward(x.cuda(), True)
+    assert eng.input.W == 64 and torch.isfinite(feat).all()
+    stem = eng.convs[0]
+    assert (stem.Ho, stem.Wo) == (32, 32)
+    xb = x.bfloat16().float()
+    Wb = stem.conv.weight.detach().cpu().bfloat16().float()
+    ref = F.conv2d(xb, Wb, None, 2, 3)
+    got = stem.out.t.detach().permute(0, 3, 1, 2).float().cpu()
+    tol = 2.0 ** -7 * ref.abs() + 1e-3 * ref.pow(2).mean().sqrt()
+    assert bool(((got - ref).abs() <= tol).all()), (got - ref).abs().max()
+    grads = {id(p): torch.zeros_like(p) for p in m.backbone.parameters()}
+    eng.backward(torch.randn(2, eng.feat_dim, device="cuda"), lambda p: grads[id(p)])
+    torch.cuda.synchronize()
+    dy = stem.out.g.detach().permute(0, 3, 1, 2).float().cpu()
+    dW = torch.nn.grad.conv2d_weight(xb, Wb.shape, dy, 2, 3)
+    err = ((grads[id(stem.conv.weight)].cpu().double() - dW.double()).norm() / dW.double().norm()).item()
+    assert err < 1e-3, err
+    # the z-CNN stem (7x7 / s2, 3 -> 32) takes the same route
+    g = PoseNetRGBGeometric(pretrained=False).cuda().set_compute_dtype(torch.bfloat16).eval()
+    K = torch.tensor([[572.4, 0, 31.0], [0, 572.4, 32.0], [0, 0, 1.0]]).expand(2, 3, 3).contiguous().cuda()
+    with torch.no_grad():
+        rot, trans = g(x.cuda(), torch.tensor([[30.0, 31.0], [10.0, 12.0]]).cuda(), K)
+    assert torch.isfinite(rot).all() and torch.isfinite(trans).all()
