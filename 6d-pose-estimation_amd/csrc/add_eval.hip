@@ -19,11 +19,11 @@
 // whenever sqrtf(new) == sqrtf(old) (same sqrt value => the old, earlier j wins).
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kPPT = 2;                       // predicted points per lane
-constexpr int kPtsPerBlock = kThreads * kPPT;
 constexpr int kTile = 2048;                   // gt points per LDS tile (32 KiB)
 
 struct Mat3 { float r[9]; };
@@ -72,61 +72,148 @@ __device__ __forceinline__ float sqdist(float ax, float ay, float az, float4 g) 
   return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
 }
 
-__global__ __launch_bounds__(kThreads) void add_points_kernel(
+// PPT predicted points per lane, U ground-truth points per loop trip: the PPT * U
+// squared distances of a trip are independent chains (3 sub, mul, 2 fma each), and
+// ONE compare-and-branch per trip asks whether any of them beat its running minimum
+// -- after the first few hundred ground-truth points almost never -- instead of a
+// branch per (point, gt point).  The rare update replays the trip's candidates in
+// ground-truth order, so every point sees its j's in the same order as the plain
+// loop: the first-index tie rule is unchanged.
+// GS wave groups of 256 threads share the block's predicted points and split every
+// ground-truth tile between them (GS times the waves per CU for the same points: the
+// loop is latency-bound at 4 waves per SIMD); the groups' minima meet in LDS at the end
+// -- the smaller sqrt wins, equal sqrt values take the smaller index, which is the
+// first index over the union (each group's index is the first in its own j's).
+template <int PPT, int U, int GS = 1, bool MINTEST = false>
+__global__ __launch_bounds__(kThreads * GS) void add_points_kernel(
     const float* __restrict__ pred_rot, const float* __restrict__ pred_trans,
     const float* __restrict__ gt_rot, const float* __restrict__ gt_trans,
     const int64_t* __restrict__ obj_ids, const float* __restrict__ points,
     const int32_t* __restrict__ off, const int32_t* __restrict__ npts, int n_slots, int max_npts,
     float* __restrict__ min_dist, int32_t* __restrict__ argmin, float* __restrict__ pt_add) {
+  constexpr int kPts = kThreads * PPT;
   __shared__ float4 gs[kTile];
+  __shared__ float mb[GS > 1 ? GS - 1 : 1][GS > 1 ? kPts : 1];
+  __shared__ int mi[GS > 1 ? GS - 1 : 1][GS > 1 ? kPts : 1];
   const int b = blockIdx.y;
   const int64_t oid = obj_ids[b];
   if (oid < 0 || oid >= n_slots) return;
   const int n = npts[oid];
-  const int base = blockIdx.x * kPtsPerBlock;
+  const int base = blockIdx.x * kPts;
   if (n <= 0 || base >= n) return;
   const Mat3 Rp = quat_to_mat(pred_rot + 4 * b);
   const Mat3 Rg = quat_to_mat(gt_rot + 4 * b);
   const float* tp = pred_trans + 3 * b;
   const float* tg = gt_trans + 3 * b;
   const float* P = points + 3 * (int64_t)off[oid];
-  const int tid = threadIdx.x;
+  const int grp = GS > 1 ? (int)threadIdx.x / kThreads : 0;
+  const int tid = (int)threadIdx.x - grp * kThreads;
 
-  float qx[kPPT], qy[kPPT], qz[kPPT], best[kPPT];
-  int bi[kPPT];
+  float qx[PPT], qy[PPT], qz[PPT], best[PPT];
+  int bi[PPT];
 #pragma unroll
-  for (int i = 0; i < kPPT; ++i) {
+  for (int i = 0; i < PPT; ++i) {
     const int k = base + tid + kThreads * i;
     best[i] = __builtin_inff();
     bi[i] = 0;
     qx[i] = qy[i] = qz[i] = 0.f;
     if (k < n) {
       const float4 q = xform(P + 3 * k, Rp, tp, n);
-      const float4 g = xform(P + 3 * k, Rg, tg, n);
       qx[i] = q.x; qy[i] = q.y; qz[i] = q.z;
-      pt_add[(int64_t)b * max_npts + k] = sqrtf(sqdist(q.x, q.y, q.z, g));  // add_loss.py:182
+      if (grp == 0) {
+        const float4 g = xform(P + 3 * k, Rg, tg, n);
+        pt_add[(int64_t)b * max_npts + k] = sqrtf(sqdist(q.x, q.y, q.z, g));  // add_loss.py:182
+      }
+    } else {
+      best[i] = -__builtin_inff();   // idle lane: nothing beats it (its result is never stored)
     }
   }
 
+  // a new squared minimum keeps the old index iff sqrtf maps both to the same value;
+  // that needs them within a few ulps (a correctly rounded sqrt of values 2^-20 apart,
+  // relative, differs by >= 8 ulps of the root), so the two square roots are taken only
+  // then -- the common update is a subtract, a multiply and a compare
+  auto update = [&](int i, float s, int j) {
+    if (s < best[i]) {
+      const float gap = best[i] - s;   // exact when the two are close (Sterbenz)
+      if (!(gap <= best[i] * 0x1p-20f) || sqrtf(s) != sqrtf(best[i])) bi[i] = j;
+      best[i] = s;
+    }
+  };
   for (int j0 = 0; j0 < n; j0 += kTile) {
     const int jn = min(kTile, n - j0);
     __syncthreads();
-    for (int jj = tid; jj < jn; jj += kThreads) gs[jj] = xform(P + 3 * (j0 + jj), Rg, tg, n);
+    for (int jj = threadIdx.x; jj < jn; jj += kThreads * GS) gs[jj] = xform(P + 3 * (j0 + jj), Rg, tg, n);
     __syncthreads();
-    for (int jj = 0; jj < jn; ++jj) {
-      const float4 g = gs[jj];
+    // this group's share of the tile
+    const int per = (jn + GS - 1) / GS;
+    const int ja = min(jn, grp * per), jb = min(jn, ja + per);
+    int jj = ja;
+    for (; jj + U <= jb; jj += U) {
+      float s[U][PPT];
+      float4 g[U];
 #pragma unroll
-      for (int i = 0; i < kPPT; ++i) {
-        const float s = sqdist(qx[i], qy[i], qz[i], g);
-        if (s < best[i]) {
-          if (sqrtf(s) != sqrtf(best[i])) bi[i] = j0 + jj;
-          best[i] = s;
+      for (int u = 0; u < U; ++u) g[u] = gs[jj + u];   // the trip's LDS reads issued together
+      // one wave-wide mask of every candidate that beats its point's minimum: each
+      // compare writes a scalar mask (ballot), the masks are OR-ed on the scalar unit and
+      // the branch is uniform -- no per-lane bit packing of the U * PPT flags
+      uint64_t hit = 0;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) s[u][i] = sqdist(qx[i], qy[i], qz[i], g[u]);
+      if constexpr (MINTEST) {
+        // min over the trip first (v_min3), one compare per point: any s < best <=> min(s) < best
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) {
+          float m = s[0][i];
+#pragma unroll
+          for (int u = 1; u < U; ++u) m = __builtin_fminf(m, s[u][i]);
+          hit |= __ballot(m < best[i]);
         }
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int i = 0; i < PPT; ++i) hit |= __ballot(s[u][i] < best[i]);
+      }
+      if (__builtin_expect(hit != 0, 0)) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int i = 0; i < PPT; ++i) update(i, s[u][i], j0 + jj + u);
       }
     }
+    for (; jj < jb; ++jj) {
+      const float4 g = gs[jj];
+#pragma unroll
+      for (int i = 0; i < PPT; ++i) update(i, sqdist(qx[i], qy[i], qz[i], g), j0 + jj);
+    }
+  }
+  if constexpr (GS > 1) {
+    if (grp > 0) {
+#pragma unroll
+      for (int i = 0; i < PPT; ++i) {
+        mb[grp - 1][tid + kThreads * i] = best[i];
+        mi[grp - 1][tid + kThreads * i] = bi[i];
+      }
+    }
+    __syncthreads();
+    if (grp > 0) return;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i)
+      for (int h = 0; h < GS - 1; ++h) {
+        const float ob = mb[h][tid + kThreads * i];
+        const int oi = mi[h][tid + kThreads * i];
+        const float so = sqrtf(ob), sm = sqrtf(best[i]);
+        if (so < sm || (so == sm && oi < bi[i])) {
+          best[i] = ob;
+          bi[i] = oi;
+        }
+      }
   }
 #pragma unroll
-  for (int i = 0; i < kPPT; ++i) {
+  for (int i = 0; i < PPT; ++i) {
     const int k = base + tid + kThreads * i;
     if (k < n) {
       min_dist[(int64_t)b * max_npts + k] = sqrtf(best[i]);  // add_loss.py:187-188
@@ -278,9 +365,32 @@ extern "C" int pose6d_add_eval(const float* pred_rot, const float* pred_trans, c
   P6_CHECK_ARG(min_dist && pt_add && add && adds && valid && correct, "pose6d_add_eval: null output");
   hipStream_t s = p6::stream_of(stream);
   if (max_npts > 0) {
-    dim3 grid(p6::ceil_div(max_npts, kPtsPerBlock), (unsigned)B);
-    add_points_kernel<<<grid, kThreads, 0, s>>>(pred_rot, pred_trans, gt_rot, gt_trans, obj_ids, points, off,
-                                                 npts, n_slots, max_npts, min_dist, argmin, pt_add);
+    static const int variant = [] {
+      const char* e = getenv("POSE6D_ADD_VARIANT");   // A/B timing only
+      return e ? atoi(e) : 0;
+    }();
+    auto go = [&](auto kern, int ppt, int gsplit) {
+      dim3 grid(p6::ceil_div(max_npts, kThreads * ppt), (unsigned)B);
+      kern<<<grid, kThreads * gsplit, 0, s>>>(pred_rot, pred_trans, gt_rot, gt_trans, obj_ids, points, off, npts,
+                                              n_slots, max_npts, min_dist, argmin, pt_add);
+    };
+    switch (variant) {
+      case 1: go(add_points_kernel<2, 1, 1>, 2, 1); break;
+      case 2: go(add_points_kernel<2, 2, 1>, 2, 1); break;
+      case 3: go(add_points_kernel<2, 4, 2>, 2, 2); break;
+      case 4: go(add_points_kernel<2, 2, 2>, 2, 2); break;
+      case 5: go(add_points_kernel<2, 4, 1>, 2, 1); break;
+      case 6: go(add_points_kernel<4, 2, 2>, 4, 2); break;
+      case 7: go(add_points_kernel<1, 4, 2>, 1, 2); break;
+      case 8: go(add_points_kernel<2, 8, 1>, 2, 1); break;
+      case 9: go(add_points_kernel<2, 4, 4>, 2, 4); break;
+      case 10: go(add_points_kernel<2, 4, 1, true>, 2, 1); break;
+      case 11: go(add_points_kernel<2, 8, 1, true>, 2, 1); break;
+      case 12: go(add_points_kernel<4, 4, 1, true>, 4, 1); break;
+      case 13: go(add_points_kernel<2, 4, 2, true>, 2, 2); break;
+      case 14: go(add_points_kernel<2, 6, 1, true>, 2, 1); break;
+      default: go(add_points_kernel<2, 4, 1>, 2, 1); break;
+    }
     P6_LAUNCH_CHECK();
   }
   add_reduce_kernel<<<(unsigned)B, kThreads, 0, s>>>(obj_ids, npts, sym, diam, n_slots, max_npts, min_dist, pt_add,

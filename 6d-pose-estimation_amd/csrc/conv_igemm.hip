@@ -1303,6 +1303,36 @@ __global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const T* __restrict_
   }
 }
 
+// The 8-wave form of the fused backward for the bf16 weight gradients on 128x128 tiles
+// (wgrad_body.h, NW = 8: twice the MACs per staged byte of the 64x64 tile; the KxK
+// convs' plans, conv_wgrad.hip): the data gradient runs on 128x64 tiles of 8 waves in
+// the same launch, the carried slab reduce on the first four waves of its workgroups
+// (the other four only meet its one barrier).
+template <int DMODE, int DS, int WS>
+__global__ __launch_bounds__(2 * kThreads) void conv_bwd8_kernel(const bf16* __restrict__ dy,
+                                                                  const bf16* __restrict__ wt,
+                                                                  const bf16* __restrict__ dres, bf16* __restrict__ dx,
+                                                                  Geom gd, int nd, int nd_pad, int wfirst,
+                                                                  const bf16* __restrict__ x, float* __restrict__ ws,
+                                                                  p6::WGeom gw, ReduceJob rj) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int b = blockIdx.x;
+  const int nw = gw.gm * gw.gn * gw.splits;
+  const int nw_pad = (nw + 7) & ~7;
+  const int d0 = wfirst ? nw_pad : 0;
+  const int w0 = wfirst ? 0 : nd_pad;
+  const int r0 = wfirst ? nw_pad + nd : nd_pad + nw;
+  if (b >= d0 && b < d0 + nd) {
+    conv_lds_body<bf16, 128, 64, DMODE, DS, false, 8, true, true>(smem, b - d0, dy, wt, nullptr, dres, dx, nullptr,
+                                                                  gd);
+  } else if (b >= w0 && b < w0 + nw) {
+    conv_wgrad_lds_body<128, 128, WS, DMODE == kGemm, false, 8>(smem, b - w0, x, dy, ws, gw);
+  } else if (b >= r0) {
+    if (threadIdx.x < kThreads) run_reduce_job(smem, b - r0, rj);
+    else __syncthreads();   // the reduce body's one workgroup barrier
+  }
+}
+
 // K-steps of the longest work item (kDgradS2: the class with the most taps);
 // ks = elements per K-step (64 bf16, 32 fp32)
 int fast_nk(int mode, const Geom& g, int ks = 64) {
@@ -1992,6 +2022,46 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
   return POSE6D_OK;
 }
 
+// the 8-wave fused launch (conv_bwd8_kernel): 128x64 data-gradient tiles, the 128x128
+// weight-gradient body on a WS-slot ring; LDS = the larger of the two roles' rings and
+// epilogue staging (the 128x128 fp32 tile staged for 16-byte slab stores: 72 KiB)
+template <int DMODE, int DS, int WS>
+int launch_bwd8(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void* wt, const void* dres, void* dx,
+                const void* x, float* ws, const ReduceJob& rj, hipStream_t s, int order) {
+  Geom gd = gd0;
+  gd.gm = p6::ceil_div(gd.M, 128);
+  gd.gn = p6::ceil_div(gd.Ncols, 64);
+  if (DMODE == kDgradS2) s2_single_class(gd, dres, dx);
+  const int nd = gd.gm * gd.gn * (DMODE == kDgradS2 ? s2_classes(gd) : 1);
+  const int nd_pad = (nd + 7) & ~7;
+  const int nw = gw.gm * gw.gn * gw.splits;
+  const int nk = fast_nk(DMODE, gd, 64);
+  const int ring_d = (nk < DS ? (nk > 0 ? nk : 1) : DS) * (128 + 64) * 128;
+  const int epi = 128 * (64 * 2 + 16) + (gd.bnr_part ? bnr_lds(8, 64) : 0);
+  const int ring_w = WS * (128 + 128) * 128;
+  int lds = ring_d > epi ? ring_d : epi;
+  lds = lds > ring_w ? lds : ring_w;
+  lds = lds > acc_stage_bytes<128, 128>() ? lds : acc_stage_bytes<128, 128>();
+  const int wfirst = order >= 0 ? order : (POSE6D_BWD_ORDER == 2 || (POSE6D_BWD_ORDER && p6::ceil_div(gw.mps, 64) >= nk));
+  const int grid = wfirst ? ((nw + 7) & ~7) + nd + rj.nblk : nd_pad + nw + rj.nblk;
+  conv_bwd8_kernel<DMODE, DS, WS><<<grid, 2 * kThreads, lds, s>>>(
+      (const bf16*)dy, (const bf16*)wt, (const bf16*)dres, (bf16*)dx, gd, nd, nd_pad, wfirst, (const bf16*)x, ws, gw,
+      rj);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+template <int DMODE>
+int launch_bwd8_mode(int ds, int ws_stages, const Geom& gd, const p6::WGeom& gw, const void* dy, const void* wt,
+                     const void* dres, void* dx, const void* x, float* ws, const ReduceJob& rj, hipStream_t s,
+                     int order) {
+  if (ws_stages >= 3)
+    return ds == 2 ? launch_bwd8<DMODE, 2, 3>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order)
+                   : launch_bwd8<DMODE, 4, 3>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order);
+  return ds == 2 ? launch_bwd8<DMODE, 2, 2>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order)
+                 : launch_bwd8<DMODE, 4, 2>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order);
+}
+
 // data-gradient ring depth of the fused launch for a plan of `stages` slots: fp32 plans
 // of 4 run 3, so that with the 32-pixel weight-gradient stages (kBwdF32MS) the launch
 // fits 48 KiB of LDS and three workgroups per CU (its VGPR budget allows three) -- the
@@ -2027,10 +2097,21 @@ int launch_bwd_mode(int dtype, int ds, const Geom& gd, const p6::WGeom& gw, cons
 // dx == NULL: weight gradient only.
 namespace {
 bool bwd_fused(int dtype, const Plan& pd, const p6::WgradPlan& pw, const pose6d_tuning_t* tn) {
-  // the fused kernel carries the 64x64 weight-gradient bodies only
-  return pd.fast && pd.tile == 3 && (pd.stages == 2 || pd.stages == 4) && pw.fast && pw.bm == 64 &&
-         pw.stages == (dtype == POSE6D_DT_BF16 ? POSE6D_WGRAD_STAGES : POSE6D_WGRAD_STAGES_F32) &&
-         tune(tn, &pose6d_tuning_t::bwd_separate, 0) == 0;
+  // the fused kernels carry the 64x64 weight-gradient bodies (conv_bwd_kernel) and the
+  // bf16 128x128 one (conv_bwd8_kernel: its data gradient on 128x64 tiles of 8 waves)
+  if (!pd.fast || pd.tile != 3 || !(pd.stages == 2 || pd.stages == 4) || !pw.fast) return false;
+  if (tune(tn, &pose6d_tuning_t::bwd_separate, 0) != 0) return false;
+  if (pw.bm == 128) return dtype == POSE6D_DT_BF16 && (pw.stages == 2 || pw.stages == 3);
+  return pw.bm == 64 && pw.stages == (dtype == POSE6D_DT_BF16 ? POSE6D_WGRAD_STAGES : POSE6D_WGRAD_STAGES_F32);
+}
+
+// the data-gradient plan a fused launch runs: the 8-wave launch (128x128 weight-gradient
+// tiles) takes 128x64 data-gradient tiles of 8 waves (tile 5), which also sets the
+// BatchNorm-reduce partial rows (bnr_plan_rows)
+Plan fused_dplan(const Plan& pd, const p6::WgradPlan& pw) {
+  Plan q = pd;
+  if (pw.bm == 128) q.tile = 5;
+  return q;
 }
 
 int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void* wt, const void* dres, void* dx,
@@ -2112,7 +2193,7 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
                "pose6d_conv2d_backward: workspace %lld bytes < %lld needed", (long long)ws_bytes,
                (long long)pw.splits * Cout * gw.Kpad * 4);
   hipStream_t s = p6::stream_of(stream);
-  int rc = check_bnr(bnr, pd, dres, dx);
+  int rc = check_bnr(bnr, fused_dplan(pd, pw), dres, dx);
   if (rc) return rc;
   Geom gd = pd.g;
   set_bnr(gd, bnr);
@@ -2127,7 +2208,19 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
   const bool direct = POSE6D_WGRAD_DIRECT && gw.splits == 1 && KH == 1 && KW == 1 && gw.Kpad == Cin &&
                       Cin_real == Cin && !accumulate;
   float* slab = direct ? dw : workspace;
-  if (phases & 1) {
+  if ((phases & 1) && pw.bm == 128) {
+    switch (pd.mode) {
+      case kGemm:
+        rc = launch_bwd8_mode<kGemm>(pd.stages, pw.stages, gd, gw, dy, wt, dres, dx, x, slab, carried, s, order);
+        break;
+      case kDgradS2:
+        rc = launch_bwd8_mode<kDgradS2>(pd.stages, pw.stages, gd, gw, dy, wt, dres, dx, x, slab, carried, s, order);
+        break;
+      default:
+        rc = launch_bwd8_mode<kDgrad>(pd.stages, pw.stages, gd, gw, dy, wt, dres, dx, x, slab, carried, s, order);
+        break;
+    }
+  } else if (phases & 1) {
     switch (pd.mode) {
       case kGemm:
         rc = launch_bwd_mode<kGemm>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, slab, carried, s, order);
@@ -2302,7 +2395,7 @@ extern "C" int pose6d_conv2d_backward_bn_rows(int32_t dtype, int32_t N, int32_t 
   const Plan pd = choose(dtype, mode, gd0, true);
   p6::WgradPlan pw;
   p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
-  return bnr_plan_rows(bwd_fused(dtype, pd, pw, nullptr) ? pd : choose(dtype, mode, gd0, false));
+  return bnr_plan_rows(bwd_fused(dtype, pd, pw, nullptr) ? fused_dplan(pd, pw) : choose(dtype, mode, gd0, false));
 }
 
 extern "C" int pose6d_conv2d_backward_chain_bn(int32_t dtype, const void* x, const void* dy, const void* wt,

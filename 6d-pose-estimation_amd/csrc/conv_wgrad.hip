@@ -245,18 +245,18 @@ int launch_reduce(const float* ws, float* dw, int Cout, int Kpad, int SC, int Ci
 
 using Plan = p6::WgradPlan;
 
-// trailing workgroups (rj.nblk) run a carried slab reduce of the previous conv
-template <int S, bool PW, bool RT>
-__global__ __launch_bounds__(kThreads) void conv_wgrad_lds_kernel(const bf16* __restrict__ x,
-                                                                  const bf16* __restrict__ dy,
-                                                                  float* __restrict__ ws, WGeom g, ReduceJob rj) {
+// trailing workgroups (rj.nblk) run a carried slab reduce of the previous conv.
+// BT = 64: 64x64 tiles on 4 waves; BT = 128: 128x128 tiles on 8 waves
+template <int S, bool PW, bool RT, int BT = 64>
+__global__ __launch_bounds__(BT == 128 ? 512 : kThreads) void conv_wgrad_lds_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ dy, float* __restrict__ ws, WGeom g, ReduceJob rj) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tiles = g.gm * g.gn;
   if ((int)blockIdx.x >= tiles * g.splits) {
-    run_reduce_job(smem, blockIdx.x - tiles * g.splits, rj);
+    if (threadIdx.x < kThreads) run_reduce_job(smem, blockIdx.x - tiles * g.splits, rj);
     return;
   }
-  conv_wgrad_lds_body<64, 64, S, PW, RT>(smem, blockIdx.x, x, dy, ws, g);
+  conv_wgrad_lds_body<BT, BT, S, PW, RT, BT == 128 ? 8 : 4>(smem, blockIdx.x, x, dy, ws, g);
 }
 
 // fp32 LDS-DMA weight gradient (wgrad_body.h conv_wgrad_lds_body_f32); trailing
@@ -341,7 +341,14 @@ int tuned(const pose6d_tuning_t* t, int32_t pose6d_tuning_t::*f, int dflt) {
 // workgroup waiting on its DMA: 56 -> 34 us graph-timed (profiles/r05w_stem_wgrad_sweep.txt).
 // The fp32 row-tap stem keeps the fp32 default (512 -> 128 splits of its 4 tiles: 147 us
 // against 156 at 256 splits and 160 register-staged, profiles/r05w32_f32_stem_wgrad.txt)
-Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* tn = nullptr, bool rowtap = false) {
+#ifndef POSE6D_WGRAD_BF128
+#define POSE6D_WGRAD_BF128 1   // build-time (A/B): 0 = the bf16 weight gradients on 64x64 tiles only
+#endif
+// wide: the geometry prefers the bf16 128x128 / 8-wave tile (KxK filters and stride-2 1x1
+// convs: graph-timed alone 24-35 % faster than 64x64 on the 3x3 convs and the 28x28
+// 512 -> 1024 downsample, slower on most stride-1 1x1 convs; profiles/r06_wgrad128_sweep.txt)
+Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* tn = nullptr, bool rowtap = false,
+          bool wide = false) {
   Plan p{};
   // wgrad_base: 0 = default, 1 = register-staged; fp32 only: 2 = LDS-DMA 64x64 tiles,
   // 3 = LDS-DMA 128x128 tiles (each where the channel counts allow it, else the default)
@@ -357,7 +364,12 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
     else if (ok64 && (Kpad == SC || Cout == 64)) f32_bt = 64;
     else if (ok128) f32_bt = POSE6D_WGRAD_F32_KXK_BT;
   }
-  p.fast = dtype == POSE6D_DT_F32 ? f32_bt != 0 : ok64 && wb == 0;
+  // bf16: wgrad_base 4 = the 128x128 / 8-wave LDS-DMA tile (Cout and the padded K multiples
+  // of 128; a 128-wide K tile may span two filter taps of 64 channels)
+  // (wgrad_base 5: the 64x64 tile wherever the default would take 128x128; tools)
+  const bool bf128 = dtype == POSE6D_DT_BF16 && (wb == 4 || (wb == 0 && wide && POSE6D_WGRAD_BF128)) && ok64 &&
+                     Cout % 128 == 0 && Kpad % 128 == 0 && !rowtap;
+  p.fast = dtype == POSE6D_DT_F32 ? f32_bt != 0 : ok64 && (wb == 0 || wb == 5 || bf128);
   int target, min_rows, step;
   int64_t max_bytes;
   if (p.fast && dtype == POSE6D_DT_F32) {
@@ -373,11 +385,11 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
     step = f32_bt == 128 ? f32_ms<128>() : f32_ms<64>();
     max_bytes = 64ll << 20;
   } else if (p.fast) {
-    p.bm = 64;
-    p.bn = 64;
-    p.stages = tuned(tn, &pose6d_tuning_t::wgrad_stages, POSE6D_WGRAD_STAGES);
+    p.bm = bf128 ? 128 : 64;
+    p.bn = bf128 ? 128 : 64;
+    p.stages = tuned(tn, &pose6d_tuning_t::wgrad_stages, bf128 ? 2 : POSE6D_WGRAD_STAGES);
     if (p.stages < 2) p.stages = 2;
-    if (p.stages > 4) p.stages = 4;
+    if (p.stages > (bf128 ? 3 : 4)) p.stages = bf128 ? 3 : 4;
     // ~256 workgroups (one per CU): with the fused launch dispatching its longest
     // workgroups first, long weight-gradient splits no longer form its tail, and
     // fewer splits write and reduce fewer fp32 slabs.  End-to-end A/B on one box
@@ -438,6 +450,19 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
 }
 
 template <int S>
+int launch_fast128(const WGeom& g, const void* x, const void* dy, float* ws, hipStream_t s, const ReduceJob& rj) {
+  int lds = S * (128 + 128) * 128;
+  if (lds < acc_stage_bytes<128, 128>()) lds = acc_stage_bytes<128, 128>();
+  const int grid = g.gm * g.gn * g.splits + rj.nblk;
+  if (g.KH == 1 && g.KW == 1 && g.stride == 1 && g.pad == 0)
+    conv_wgrad_lds_kernel<S, true, false, 128><<<grid, 512, lds, s>>>((const bf16*)x, (const bf16*)dy, ws, g, rj);
+  else
+    conv_wgrad_lds_kernel<S, false, false, 128><<<grid, 512, lds, s>>>((const bf16*)x, (const bf16*)dy, ws, g, rj);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+template <int S>
 int launch_fast(const WGeom& g, const void* x, const void* dy, float* ws, hipStream_t s,
                 const ReduceJob& rj = ReduceJob{}) {
   static_assert(S * (64 + 64) * 128 >= acc_stage_bytes<64, 64>(), "ring too small to stage the tile");
@@ -455,6 +480,7 @@ int launch_fast(const WGeom& g, const void* x, const void* dy, float* ws, hipStr
 
 int launch_fast_any(const Plan& p, const WGeom& g, const void* x, const void* dy, float* ws, hipStream_t s,
                     const ReduceJob& rj = ReduceJob{}) {
+  if (p.bm == 128) return p.stages == 3 ? launch_fast128<3>(g, x, dy, ws, s, rj) : launch_fast128<2>(g, x, dy, ws, s, rj);
   return p.stages == 2 ? launch_fast<2>(g, x, dy, ws, s, rj)
        : p.stages == 3 ? launch_fast<3>(g, x, dy, ws, s, rj)
                        : launch_fast<4>(g, x, dy, ws, s, rj);
@@ -495,9 +521,14 @@ extern "C" int64_t pose6d_conv2d_wgrad_workspace_tuned(int32_t dtype, int32_t N,
   const int K = KH * KW * Cin;
   int64_t need = 0;
   {
+    // (the stride is not an argument: a 1x1 conv may take the wide plan too (stride 2) --
+    // report the larger of the two)
     const int Kpad = p6::ceil_div(K, bk) * bk;
-    const Plan p = plan(dtype, N * Ho * Wo, Cout, Kpad, Cin, tuning);
-    need = (int64_t)p.splits * Cout * Kpad * 4;
+    for (int wide = 0; wide < 2; ++wide) {
+      const Plan p = plan(dtype, N * Ho * Wo, Cout, Kpad, Cin, tuning, false, wide != 0);
+      const int64_t b = (int64_t)p.splits * Cout * Kpad * 4;
+      if (b > need) need = b;
+    }
   }
   // (the stride / padding are not arguments: a 4-channel stem may take the row-tap plan,
   // whose slabs are wider -- report the larger of the two)
@@ -540,7 +571,7 @@ WGeom wgrad_geom(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int 
       return g;
     }
   }
-  const Plan p = plan(dtype, g.M, Cout, g.Kpad, Cin, tuning);
+  const Plan p = plan(dtype, g.M, Cout, g.Kpad, Cin, tuning, false, KH * KW > 1 || stride > 1);
   g.gm = ceil_div(Cout, p.bm); g.gn = ceil_div(g.Kpad, p.bn);
   g.splits = p.splits; g.mps = p.mps;
   if (plan_out) *plan_out = p;

@@ -66,14 +66,16 @@ namespace {
 template <int BM, int BN>
 constexpr int acc_stage_bytes() { return BM * (BN + 16) * 4; }
 
-template <int BM, int BN, bool CHECK>
-__device__ __forceinline__ void store_acc_tile(const f32x4 (&acc)[BM / 32][BN / 32], char* smem, float* dst,
-                                               int64_t ld, int rows, int cols) {
-  constexpr int TM = BM / 32, TN = BN / 32;
+template <int BM, int BN, bool CHECK, int NW = 4>
+__device__ __forceinline__ void store_acc_tile(const f32x4 (&acc)[BM / 32][BN / (8 * NW)],
+                                               char* smem, float* dst, int64_t ld, int rows, int cols) {
+  // wave grid WM x WN = 2 x (NW / 2): each wave holds BM / WM rows x BN / WN columns
+  constexpr int WM = 2, WN = NW / 2, NT = 64 * NW;
+  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
   constexpr int LDT = BN + 16;              // floats per LDS row: rows alternate 16-bank halves
   float* t = reinterpret_cast<float*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int grp = lane >> 4, li = lane & 15;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -81,10 +83,10 @@ __device__ __forceinline__ void store_acc_tile(const f32x4 (&acc)[BM / 32][BN / 
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        t[(wm * (BM / 2) + i * 16 + grp * 4 + r) * LDT + wn * (BN / 2) + j * 16 + li] = acc[i][j][r];
+        t[(wm * (BM / WM) + i * 16 + grp * 4 + r) * LDT + wn * (BN / WN) + j * 16 + li] = acc[i][j][r];
   __syncthreads();
   constexpr int CPR = BN / 4;               // float4 per row
-  constexpr int RPP = 256 / CPR;            // rows per pass
+  constexpr int RPP = NT / CPR;             // rows per pass
   const int c4 = tid % CPR, r0 = tid / CPR;
 #pragma unroll
   for (int pass = 0; pass < BM / RPP; ++pass) {
@@ -155,16 +157,22 @@ __device__ __forceinline__ void lds_wait_tr8(u32x2 (&f)[8]) {
 // RT: the row-tap X image (the 4-channel 7x7 / stride-2 stems, common.h): sub-image
 // s of a stage is the slab's K columns [k0 + 64 s, + 64) = two kernel rows x 8 taps x 4
 // channels, i.e. each X row is two 64-byte runs of 8 input pixels
-template <int BM, int BN, int S, bool PW = false, bool RT = false>
+// NW: waves per workgroup, as a 2 x NW/2 grid over the (BM co) x (BN k) tile -- 4 (64x64
+// tiles: 32 x 32 per wave) or 8 (128x128 tiles: 64 x 32 per wave, twice the MACs per
+// staged byte of the 64x64 tile and half the DMA instructions per wave per byte)
+template <int BM, int BN, int S, bool PW = false, bool RT = false, int NW = 4>
 __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const bf16* __restrict__ x,
                                                     const bf16* __restrict__ dy, float* __restrict__ ws,
                                                     const p6::WGeom& g) {
   constexpr int MS = 64;                          // pixels per stage
   constexpr int YS = BM / 64, XS = BN / 64;       // 64-column sub-images per operand
-  constexpr int LOADS = 2 * (YS + XS);            // DMA instructions per thread per stage
+  constexpr int RI = 64 / (8 * NW);               // DMA rows of a sub-image per thread (8 rows per wave instruction)
+  constexpr int LOADS = RI * (YS + XS);           // DMA instructions per thread per stage
   constexpr int SUB = MS * 128;                   // bytes per sub-image
   constexpr int STAGE = (YS + XS) * SUB;
-  constexpr int TM = BM / 32, TN = BN / 32;
+  constexpr int WM = 2, WN = NW / 2;
+  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert((TM + TN) % 2 == 0 && TM + TN <= 8, "fragment batches of 2 or 4 operands");
 
   const int tiles = g.gm * g.gn;
@@ -180,16 +188,16 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
   const int mbeg = split * g.mps;
   const int mend = min(g.M, mbeg + g.mps);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int r8 = lane >> 3, pch = lane & 7;
   const char* zp = reinterpret_cast<const char*>(g_zero_page);
   constexpr bool pointwise = PW;
 
-  // each thread DMAs rows R = i * 32 + wave * 8 + r8 (i = 0, 1) of every sub-image;
+  // each thread DMAs rows R = i * 8 NW + wave * 8 + r8 (i < RI) of every sub-image;
   // the logical chunk it fetches carries the row's swizzle
-  int ck[2];
+  int ck[RI];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) ck[i] = (pch ^ swz_tr4(i * 32 + wave * 8 + r8)) * 8;
+  for (int i = 0; i < RI; ++i) ck[i] = (pch ^ swz_tr4(i * 8 * NW + wave * 8 + r8)) * 8;
   int tap_h[XS], tap_w[XS], ci0[XS];
 #pragma unroll
   for (int s = 0; s < XS; ++s) {
@@ -203,11 +211,11 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
   // stage without divisions (issue() is called with consecutive st)
   const int hw = g.RH * g.RW;
   const int step_y = MS / g.RW, step_x = MS - step_y * g.RW;
-  int rn[2], roy[2], rox[2];
+  int rn[RI], roy[RI], rox[RI];
   if (!pointwise) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int m = mbeg + i * 32 + wave * 8 + r8;
+    for (int i = 0; i < RI; ++i) {
+      const int m = mbeg + i * 8 * NW + wave * 8 + r8;
       rn[i] = m / hw;
       const int rem = m - rn[i] * hw;
       roy[i] = rem / g.RW;
@@ -216,13 +224,13 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
   }
 
   // pointwise: per-row operand pointers advanced by a stage each issue
-  const bf16* pw_y[2][YS];
-  const bf16* pw_x[2][XS];
-  int pw_m[2];
+  const bf16* pw_y[RI][YS];
+  const bf16* pw_x[RI][XS];
+  int pw_m[RI];
   if constexpr (PW) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int m = mbeg + i * 32 + wave * 8 + r8;
+    for (int i = 0; i < RI; ++i) {
+      const int m = mbeg + i * 8 * NW + wave * 8 + r8;
       pw_m[i] = m;
 #pragma unroll
       for (int s_ = 0; s_ < YS; ++s_) pw_y[i][s_] = dy + (int64_t)m * g.Cout + co0 + s_ * 64 + ck[i];
@@ -236,14 +244,15 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
     char* base = smem + buf * STAGE;
     if constexpr (PW) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < RI; ++i) {
         const bool ok = pw_m[i] < mend;
 #pragma unroll
         for (int s_ = 0; s_ < YS; ++s_)
-          glds16(ok ? (const void*)pw_y[i][s_] : (const void*)zp, base + s_ * SUB + (i * 32 + wave * 8) * 128);
+          glds16(ok ? (const void*)pw_y[i][s_] : (const void*)zp, base + s_ * SUB + (i * 8 * NW + wave * 8) * 128);
 #pragma unroll
         for (int s_ = 0; s_ < XS; ++s_)
-          glds16(ok ? (const void*)pw_x[i][s_] : (const void*)zp, base + (YS + s_) * SUB + (i * 32 + wave * 8) * 128);
+          glds16(ok ? (const void*)pw_x[i][s_] : (const void*)zp,
+                 base + (YS + s_) * SUB + (i * 8 * NW + wave * 8) * 128);
         pw_m[i] += MS;
 #pragma unroll
         for (int s_ = 0; s_ < YS; ++s_) pw_y[i][s_] += y_step;
@@ -254,14 +263,14 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
       return;
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int R = i * 32 + wave * 8 + r8;
+    for (int i = 0; i < RI; ++i) {
+      const int R = i * 8 * NW + wave * 8 + r8;
       const int m = mbeg + st * MS + R;
       const bool ok = m < mend;
 #pragma unroll
       for (int s = 0; s < YS; ++s) {
         const void* p = ok ? (const void*)(dy + (int64_t)m * g.Cout + co0 + s * 64 + ck[i]) : (const void*)zp;
-        glds16(p, base + s * SUB + (i * 32 + wave * 8) * 128);
+        glds16(p, base + s * SUB + (i * 8 * NW + wave * 8) * 128);
       }
       int sy = 0, sx = 0;
       if (!pointwise) {
@@ -284,7 +293,7 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
           if (ok && (unsigned)yy < (unsigned)g.SH && (unsigned)xx < (unsigned)g.SW)
             p = x + ((((int64_t)rn[i] * g.SH + yy) * g.SW + xx) << g.log2SC) + ci0[s] + ck[i];
         }
-        glds16(p, base + (YS + s) * SUB + (i * 32 + wave * 8) * 128);
+        glds16(p, base + (YS + s) * SUB + (i * 8 * NW + wave * 8) * 128);
       }
       if (!pointwise) {
         rox[i] += step_x;
@@ -311,7 +320,7 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const bool isy = o < TM;
-        const int col = isy ? wm * (BM / 2) + o * 16 + 4 * p : wn * (BN / 2) + (o - TM) * 16 + 4 * p;
+        const int col = isy ? wm * (BM / WM) + o * 16 + 4 * p : wn * (BN / WN) + (o - TM) * 16 + 4 * p;
         const int sub = (isy ? 0 : YS) + (col >> 6), lc = col & 63;
         const int r = 32 * kk + 8 * grp + 4 * h + q;
         off[kk][2 * o + h] = sub * SUB + r * 128 + (((lc >> 3) ^ swz_tr4(r)) << 4) + (lc & 7) * 2;
@@ -323,7 +332,7 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       u32x2 f[2 * (TM + TN)];
-      constexpr int NB = TM + TN >= 4 ? 4 : 2;   // operands per asm batch
+      constexpr int NB = (TM + TN) % 4 == 0 ? 4 : 2;   // operands per asm batch
 #pragma unroll
       for (int b0 = 0; b0 < TM + TN; b0 += NB) {
         unsigned a[2 * NB];
@@ -376,7 +385,7 @@ __device__ __forceinline__ void conv_wgrad_lds_body(char* smem, int bid, const b
   // wait_ahead waited for all of them) before the tile is staged over it
   asm volatile("s_barrier" ::: "memory");
   float* slab = ws + (int64_t)split * g.Cout * g.Kpad;
-  store_acc_tile<BM, BN, false>(acc, smem, slab + (int64_t)co0 * g.Kpad + k0, g.Kpad, BM, BN);
+  store_acc_tile<BM, BN, false, NW>(acc, smem, slab + (int64_t)co0 * g.Kpad + k0, g.Kpad, BM, BN);
 }
 
 
