@@ -7,8 +7,9 @@
 //                      meshes left 2 waves per SIMD and the loop latency-bound; at 1,
 //                      every gt tile is transformed and read for half the work), streams that sample's
 //                      transformed ground-truth mesh through LDS in 2048-point tiles
-//                      (broadcast ds_read_b128, no bank conflicts) and keeps a running
-//                      nearest-point minimum per predicted point in registers.
+//                      (broadcast reads, no bank conflicts) and keeps a running
+//                      nearest-point minimum per predicted point in registers: 4 gt
+//                      points per trip, one scalar branch per trip (round 6).
 //   add_reduce_kernel  grid B: fixed-order fp64 means (deterministic), 0.1d test.
 //
 // Bit-exactness contract (pinned by tests/golden/add_loss.npz):
@@ -18,8 +19,6 @@
 // FIRST index among equal values, so a new squared minimum keeps the old index
 // whenever sqrtf(new) == sqrtf(old) (same sqrt value => the old, earlier j wins).
 #include "common.h"
-
-#include <stdlib.h>
 
 namespace {
 
@@ -79,13 +78,8 @@ __device__ __forceinline__ float sqdist(float ax, float ay, float az, float4 g) 
 // branch per (point, gt point).  The rare update replays the trip's candidates in
 // ground-truth order, so every point sees its j's in the same order as the plain
 // loop: the first-index tie rule is unchanged.
-// GS wave groups of 256 threads share the block's predicted points and split every
-// ground-truth tile between them (GS times the waves per CU for the same points: the
-// loop is latency-bound at 4 waves per SIMD); the groups' minima meet in LDS at the end
-// -- the smaller sqrt wins, equal sqrt values take the smaller index, which is the
-// first index over the union (each group's index is the first in its own j's).
-template <int PPT, int U, int GS = 1, bool MINTEST = false>
-__global__ __launch_bounds__(kThreads * GS) void add_points_kernel(
+template <int PPT, int U>
+__global__ __launch_bounds__(kThreads) void add_points_kernel(
     const float* __restrict__ pred_rot, const float* __restrict__ pred_trans,
     const float* __restrict__ gt_rot, const float* __restrict__ gt_trans,
     const int64_t* __restrict__ obj_ids, const float* __restrict__ points,
@@ -93,8 +87,6 @@ __global__ __launch_bounds__(kThreads * GS) void add_points_kernel(
     float* __restrict__ min_dist, int32_t* __restrict__ argmin, float* __restrict__ pt_add) {
   constexpr int kPts = kThreads * PPT;
   __shared__ float4 gs[kTile];
-  __shared__ float mb[GS > 1 ? GS - 1 : 1][GS > 1 ? kPts : 1];
-  __shared__ int mi[GS > 1 ? GS - 1 : 1][GS > 1 ? kPts : 1];
   const int b = blockIdx.y;
   const int64_t oid = obj_ids[b];
   if (oid < 0 || oid >= n_slots) return;
@@ -106,8 +98,7 @@ __global__ __launch_bounds__(kThreads * GS) void add_points_kernel(
   const float* tp = pred_trans + 3 * b;
   const float* tg = gt_trans + 3 * b;
   const float* P = points + 3 * (int64_t)off[oid];
-  const int grp = GS > 1 ? (int)threadIdx.x / kThreads : 0;
-  const int tid = (int)threadIdx.x - grp * kThreads;
+  const int tid = threadIdx.x;
 
   float qx[PPT], qy[PPT], qz[PPT], best[PPT];
   int bi[PPT];
@@ -120,10 +111,8 @@ __global__ __launch_bounds__(kThreads * GS) void add_points_kernel(
     if (k < n) {
       const float4 q = xform(P + 3 * k, Rp, tp, n);
       qx[i] = q.x; qy[i] = q.y; qz[i] = q.z;
-      if (grp == 0) {
-        const float4 g = xform(P + 3 * k, Rg, tg, n);
-        pt_add[(int64_t)b * max_npts + k] = sqrtf(sqdist(q.x, q.y, q.z, g));  // add_loss.py:182
-      }
+      const float4 g = xform(P + 3 * k, Rg, tg, n);
+      pt_add[(int64_t)b * max_npts + k] = sqrtf(sqdist(q.x, q.y, q.z, g));  // add_loss.py:182
     } else {
       best[i] = -__builtin_inff();   // idle lane: nothing beats it (its result is never stored)
     }
@@ -143,39 +132,29 @@ __global__ __launch_bounds__(kThreads * GS) void add_points_kernel(
   for (int j0 = 0; j0 < n; j0 += kTile) {
     const int jn = min(kTile, n - j0);
     __syncthreads();
-    for (int jj = threadIdx.x; jj < jn; jj += kThreads * GS) gs[jj] = xform(P + 3 * (j0 + jj), Rg, tg, n);
+    for (int jj = tid; jj < jn; jj += kThreads) gs[jj] = xform(P + 3 * (j0 + jj), Rg, tg, n);
     __syncthreads();
-    // this group's share of the tile
-    const int per = (jn + GS - 1) / GS;
-    const int ja = min(jn, grp * per), jb = min(jn, ja + per);
-    int jj = ja;
-    for (; jj + U <= jb; jj += U) {
+    int jj = 0;
+    for (; jj + U <= jn; jj += U) {
       float s[U][PPT];
       float4 g[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) g[u] = gs[jj + u];   // the trip's LDS reads issued together
-      // one wave-wide mask of every candidate that beats its point's minimum: each
-      // compare writes a scalar mask (ballot), the masks are OR-ed on the scalar unit and
-      // the branch is uniform -- no per-lane bit packing of the U * PPT flags
+      // one wave-wide mask of the points that have a candidate beating their minimum:
+      // each compare writes a scalar mask (ballot), the masks are OR-ed on the scalar
+      // unit and the branch is uniform -- no per-lane bit packing of the flags
       uint64_t hit = 0;
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int i = 0; i < PPT; ++i) s[u][i] = sqdist(qx[i], qy[i], qz[i], g[u]);
-      if constexpr (MINTEST) {
-        // min over the trip first (v_min3), one compare per point: any s < best <=> min(s) < best
+      // min over the trip first (v_min3), one compare per point: any s < best <=> min(s) < best
 #pragma unroll
-        for (int i = 0; i < PPT; ++i) {
-          float m = s[0][i];
+      for (int i = 0; i < PPT; ++i) {
+        float m = s[0][i];
 #pragma unroll
-          for (int u = 1; u < U; ++u) m = __builtin_fminf(m, s[u][i]);
-          hit |= __ballot(m < best[i]);
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-          for (int i = 0; i < PPT; ++i) hit |= __ballot(s[u][i] < best[i]);
+        for (int u = 1; u < U; ++u) m = __builtin_fminf(m, s[u][i]);
+        hit |= __ballot(m < best[i]);
       }
       if (__builtin_expect(hit != 0, 0)) {
 #pragma unroll
@@ -184,33 +163,11 @@ __global__ __launch_bounds__(kThreads * GS) void add_points_kernel(
           for (int i = 0; i < PPT; ++i) update(i, s[u][i], j0 + jj + u);
       }
     }
-    for (; jj < jb; ++jj) {
+    for (; jj < jn; ++jj) {
       const float4 g = gs[jj];
 #pragma unroll
       for (int i = 0; i < PPT; ++i) update(i, sqdist(qx[i], qy[i], qz[i], g), j0 + jj);
     }
-  }
-  if constexpr (GS > 1) {
-    if (grp > 0) {
-#pragma unroll
-      for (int i = 0; i < PPT; ++i) {
-        mb[grp - 1][tid + kThreads * i] = best[i];
-        mi[grp - 1][tid + kThreads * i] = bi[i];
-      }
-    }
-    __syncthreads();
-    if (grp > 0) return;
-#pragma unroll
-    for (int i = 0; i < PPT; ++i)
-      for (int h = 0; h < GS - 1; ++h) {
-        const float ob = mb[h][tid + kThreads * i];
-        const int oi = mi[h][tid + kThreads * i];
-        const float so = sqrtf(ob), sm = sqrtf(best[i]);
-        if (so < sm || (so == sm && oi < bi[i])) {
-          best[i] = ob;
-          bi[i] = oi;
-        }
-      }
   }
 #pragma unroll
   for (int i = 0; i < PPT; ++i) {
@@ -365,32 +322,15 @@ extern "C" int pose6d_add_eval(const float* pred_rot, const float* pred_trans, c
   P6_CHECK_ARG(min_dist && pt_add && add && adds && valid && correct, "pose6d_add_eval: null output");
   hipStream_t s = p6::stream_of(stream);
   if (max_npts > 0) {
-    static const int variant = [] {
-      const char* e = getenv("POSE6D_ADD_VARIANT");   // A/B timing only
-      return e ? atoi(e) : 0;
-    }();
-    auto go = [&](auto kern, int ppt, int gsplit) {
-      dim3 grid(p6::ceil_div(max_npts, kThreads * ppt), (unsigned)B);
-      kern<<<grid, kThreads * gsplit, 0, s>>>(pred_rot, pred_trans, gt_rot, gt_trans, obj_ids, points, off, npts,
-                                              n_slots, max_npts, min_dist, argmin, pt_add);
-    };
-    switch (variant) {
-      case 1: go(add_points_kernel<2, 1, 1>, 2, 1); break;
-      case 2: go(add_points_kernel<2, 2, 1>, 2, 1); break;
-      case 3: go(add_points_kernel<2, 4, 2>, 2, 2); break;
-      case 4: go(add_points_kernel<2, 2, 2>, 2, 2); break;
-      case 5: go(add_points_kernel<2, 4, 1>, 2, 1); break;
-      case 6: go(add_points_kernel<4, 2, 2>, 4, 2); break;
-      case 7: go(add_points_kernel<1, 4, 2>, 1, 2); break;
-      case 8: go(add_points_kernel<2, 8, 1>, 2, 1); break;
-      case 9: go(add_points_kernel<2, 4, 4>, 2, 4); break;
-      case 10: go(add_points_kernel<2, 4, 1, true>, 2, 1); break;
-      case 11: go(add_points_kernel<2, 8, 1, true>, 2, 1); break;
-      case 12: go(add_points_kernel<4, 4, 1, true>, 4, 1); break;
-      case 13: go(add_points_kernel<2, 4, 2, true>, 2, 2); break;
-      case 14: go(add_points_kernel<2, 6, 1, true>, 2, 1); break;
-      default: go(add_points_kernel<2, 4, 1>, 2, 1); break;
-    }
+    // 2 predicted points per lane, 4 ground-truth points per trip: A/B on one box
+    // (tools/add_ab.py, profiles/r06_add_variants.txt) -- 4 points per lane, 6 or 8 gt
+    // points per trip, or 2-4 wave groups of one block splitting the ground truth (twice
+    // the waves per SIMD) were all slower
+    constexpr int kPPT = 2;
+    dim3 grid(p6::ceil_div(max_npts, kThreads * kPPT), (unsigned)B);
+    add_points_kernel<kPPT, 4><<<grid, kThreads, 0, s>>>(pred_rot, pred_trans, gt_rot, gt_trans, obj_ids,
+                                                                   points, off, npts, n_slots, max_npts, min_dist,
+                                                                   argmin, pt_add);
     P6_LAUNCH_CHECK();
   }
   add_reduce_kernel<<<(unsigned)B, kThreads, 0, s>>>(obj_ids, npts, sym, diam, n_slots, max_npts, min_dist, pt_add,

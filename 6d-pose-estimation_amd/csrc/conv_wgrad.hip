@@ -342,7 +342,7 @@ int tuned(const pose6d_tuning_t* t, int32_t pose6d_tuning_t::*f, int dflt) {
 // The fp32 row-tap stem keeps the fp32 default (512 -> 128 splits of its 4 tiles: 147 us
 // against 156 at 256 splits and 160 register-staged, profiles/r05w32_f32_stem_wgrad.txt)
 #ifndef POSE6D_WGRAD_BF128
-#define POSE6D_WGRAD_BF128 1   // build-time (A/B): 0 = the bf16 weight gradients on 64x64 tiles only
+#define POSE6D_WGRAD_BF128 1   // build-time (A/B): 0 = the bf16 weight gradients on 64x64 tiles only, 2 = 128x128 wherever eligible
 #endif
 // wide: the geometry prefers the bf16 128x128 / 8-wave tile (KxK filters and stride-2 1x1
 // convs: graph-timed alone 24-35 % faster than 64x64 on the 3x3 convs and the 28x28
@@ -367,7 +367,8 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
   // bf16: wgrad_base 4 = the 128x128 / 8-wave LDS-DMA tile (Cout and the padded K multiples
   // of 128; a 128-wide K tile may span two filter taps of 64 channels)
   // (wgrad_base 5: the 64x64 tile wherever the default would take 128x128; tools)
-  const bool bf128 = dtype == POSE6D_DT_BF16 && (wb == 4 || (wb == 0 && wide && POSE6D_WGRAD_BF128)) && ok64 &&
+  const bool bf128 = dtype == POSE6D_DT_BF16 &&
+                     (wb == 4 || (wb == 0 && (POSE6D_WGRAD_BF128 == 2 || (wide && POSE6D_WGRAD_BF128)))) && ok64 &&
                      Cout % 128 == 0 && Kpad % 128 == 0 && !rowtap;
   p.fast = dtype == POSE6D_DT_F32 ? f32_bt != 0 : ok64 && (wb == 0 || wb == 5 || bf128);
   int target, min_rows, step;
