@@ -54,25 +54,14 @@ __device__ __forceinline__ void store_vec(T* p, const float* f) {
 // deterministic), and mean = K + S1/N, var = (S2 - S1^2/N)/N.  The shift keeps
 // S1^2/N small against S2 (K is a mean of the same data): no E[x^2]-E[x]^2
 // cancellation.
+// lane l (of L on channel c) folds rows l, l + L, ...; after the call thread `lane == 0`
+// of the channel holds (K, s1, s2) of the whole channel (L = 256: thread 0 of the block)
 template <int L>
-__device__ __forceinline__ void bn_stats_finalize_body(
-    int blk, const float* __restrict__ part, int rows, int C, int64_t M, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
-    float momentum, float eps, float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ smean,
-    float* __restrict__ sinv) {
+__device__ __forceinline__ void bn_stats_fold(const float* __restrict__ part, int rows, int C, int64_t M, int c,
+                                              double& K, double& s1, double& s2) {
   __shared__ double red[2][kThreads / 64];
   const int lane = threadIdx.x % L;
-  const int c = blk * (kThreads / L) + threadIdx.x / L;
-  double s1 = 0.0, s2 = 0.0, K = 0.0;
-  // the per-channel parameters and running statistics the tail needs, fetched now
-  // so their round trip overlaps the partial-row reduction instead of following it
-  float g_c = 0.f, b_c = 0.f, rm_c = 0.f, rv_c = 0.f;
-  if (lane == 0 && c < C) {
-    g_c = gamma[c];
-    b_c = beta[c];
-    rm_c = rmean[c];
-    rv_c = rvar[c];
-  }
+  s1 = 0.0; s2 = 0.0; K = 0.0;
   if (c < C) {
     const float* ps = part + (int64_t)c * rows;          // channel-major partials: coalesced rows
     const float* pq = part + ((int64_t)C + c) * rows;
@@ -108,6 +97,7 @@ __device__ __forceinline__ void bn_stats_finalize_body(
   s2 = p6::wave_sum(s2);
   if constexpr (L > 64) {
     const int w = threadIdx.x >> 6;
+    __syncthreads();   // (red reused across calls)
     if ((threadIdx.x & 63) == 0) { red[0][w] = s1; red[1][w] = s2; }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -116,19 +106,41 @@ __device__ __forceinline__ void bn_stats_finalize_body(
       for (int i = 0; i < kThreads / 64; ++i) { s1 += red[0][i]; s2 += red[1][i]; }
     }
   }
+}
+
+template <int L, bool SC1 = false>
+__device__ __forceinline__ void bn_stats_finalize_body(
+    int blk, const float* __restrict__ part, int rows, int C, int64_t M, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
+    float momentum, float eps, float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ smean,
+    float* __restrict__ sinv) {
+  const int lane = threadIdx.x % L;
+  const int c = blk * (kThreads / L) + threadIdx.x / L;
+  // the per-channel parameters and running statistics the tail needs, fetched now
+  // so their round trip overlaps the partial-row reduction instead of following it
+  float g_c = 0.f, b_c = 0.f, rm_c = 0.f, rv_c = 0.f;
   if (lane == 0 && c < C) {
+    g_c = gamma[c];
+    b_c = beta[c];
+    rm_c = rmean[c];
+    rv_c = rvar[c];
+  }
+  double K, s1, s2;
+  bn_stats_fold<L>(part, rows, C, M, c, K, s1, s2);
+  if (lane == 0 && c < C) {
+    const p6::BnFoldOut o = p6::bn_fold_result(M, eps, K, s1, s2, g_c, b_c);
     const double N = (double)M;
-    const double mean = K + s1 / N;
-    double var = (s2 - s1 * s1 / N) / N;
-    if (var < 0.0) var = 0.0;
-    const float inv = (float)(1.0 / sqrt(var + (double)eps));
-    const float sc = g_c * inv;
-    scale[c] = sc;
-    shift[c] = b_c - (float)mean * sc;
-    smean[c] = (float)mean;
-    sinv[c] = inv;
-    const double unb = N > 1.0 ? var * N / (N - 1.0) : var;
-    rmean[c] = (1.f - momentum) * rm_c + momentum * (float)mean;
+    if constexpr (SC1) {
+      p6::st_sc1(scale, c, o.sc);
+      p6::st_sc1(shift, c, o.sh);
+    } else {
+      scale[c] = o.sc;
+      shift[c] = o.sh;
+    }
+    smean[c] = (float)o.mean;
+    sinv[c] = o.inv;
+    const double unb = N > 1.0 ? o.var * N / (N - 1.0) : o.var;
+    rmean[c] = (1.f - momentum) * rm_c + momentum * (float)o.mean;
     rvar[c] = (1.f - momentum) * rv_c + momentum * (float)unb;
     if (c == 0 && nbt) nbt[0] += 1;
   }
@@ -248,6 +260,141 @@ __global__ __launch_bounds__(kThreads) void bn_act_kernel(const T* __restrict__ 
       for (int e = 0; e < E; ++e) b |= (p6::to_f(p6::from_f<T>(v[e])) > 0.f ? 1u : 0u) << e;
       mbits[i] = (uint8_t)b;
     }
+  }
+}
+
+// ---------------------------------------------------------------- finalize + apply, one launch
+// pose6d_bn_finalize_act: the training finalize and bn_act_kernel's apply in ONE launch
+// (the kernel boundary between them -- a launch gap plus the apply's ramp behind a
+// ~5 us latency-bound finalize -- is what the separate launches cost).  Workgroups
+// [0, nfin) are the finalize (bn_stats_finalize_kernel<L>'s blocks, same arithmetic),
+// each storing scale / shift write-through and then ITS ready flag (= the launch's
+// epoch).  Workgroups [nfin, ...) apply: one 64-channel column group x RPB rows each;
+// they fetch their y / residual chunks first, then one wave polls the flags of the
+// finalize workgroups that cover its 64 channels (sc1 loads, bounded), reads scale /
+// shift write-through and stores bn_act_kernel's result bit for bit.  Nothing assumes
+// a dispatch order: an apply workgroup that does not see its flags within kFinSpins
+// polls folds its 64 channels itself (the finalize's arithmetic, same bits) -- slow,
+// never wrong, never a hang.
+constexpr int kFinGroup = 64;     // channels per apply column group
+constexpr int kFinSpins = 4096;   // ~4096 x (poll + s_sleep 2) ~ 0.5 ms before the fallback
+
+template <int L>
+__device__ __forceinline__ int fin_blocks(int C) { return L == 64 ? (C + 3) / 4 : C; }
+
+// the 64 channels' scale / shift into LDS for a workgroup that gave up waiting: the
+// finalize's fold recomputed (rows <= 512: one wave per 16 channels, bn_fold.h; more
+// rows: the whole workgroup per channel, bn_stats_fold<256>)
+template <int L>
+__device__ void fin_fallback(const pose6d_bn_stats_t& d, int rows, int64_t M, int c0, float* sc, float* sh) {
+  if constexpr (L == 64) {
+    const int w = threadIdx.x >> 6;
+    p6::bn_fold_wave_compute(d, rows, M, c0 + 16 * w, 16, sc + 16 * w, sh + 16 * w);
+  } else {
+    for (int j = 0; j < kFinGroup; ++j) {
+      double K, s1, s2;
+      bn_stats_fold<256>(d.partial, rows, d.C, M, c0 + j, K, s1, s2);
+      if (threadIdx.x == 0 && c0 + j < d.C) {
+        const p6::BnFoldOut o = p6::bn_fold_result(M, d.eps, K, s1, s2, d.gamma[c0 + j], d.beta[c0 + j]);
+        sc[j] = o.sc;
+        sh[j] = o.sh;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+template <typename T, int L>
+__global__ __launch_bounds__(kThreads) void bn_fin_act_kernel(pose6d_bn_stats_t d, int rows, int64_t M, int nfin,
+                                                              const T* __restrict__ y, const T* __restrict__ res,
+                                                              int relu, T* __restrict__ out,
+                                                              uint8_t* __restrict__ mbits, int* __restrict__ flags,
+                                                              const int64_t* __restrict__ epoch) {
+  __shared__ float csc[kFinGroup], csh[kFinGroup];
+  __shared__ int fb;
+  const int64_t e64 = epoch[0];
+  const int ep = (int)(e64 & 0x3fffffff) + 1;   // flags start at 0; never equal to a fresh epoch's value
+  const int b = blockIdx.x;
+  const int C = d.C;
+  if (b < nfin) {
+    // ---- finalize: bn_stats_finalize_kernel<L>'s workgroup b, scale / shift written through
+    if constexpr (L == 64) {
+      const float* part = d.partial;
+      p6::bn_fold_wave<1, p6::kBnFoldSlots, true>(d, [&](int64_t i) { return part[i]; }, rows, M,
+                                                   b * 4 + (threadIdx.x >> 6), 1);
+    } else {
+      bn_stats_finalize_body<L, true>(b, d.partial, rows, C, M, d.gamma, d.beta, d.running_mean, d.running_var,
+                                      d.num_batches, d.momentum, d.eps, d.scale, d.shift, d.save_mean,
+                                      d.save_invstd);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave, before the barrier
+    __syncthreads();
+    if (threadIdx.x == 0) p6::st_sc1(flags, b, ep);
+    return;
+  }
+  // ---- apply: column group g (64 channels), rows [rb * RPB, + RPB)
+  constexpr int E = V<T>::E;
+  constexpr int CPS = kFinGroup / E;     // 16-byte chunks per row of a group
+  constexpr int RPB = kThreads / CPS;    // rows per workgroup
+  const int ng = C / kFinGroup;
+  const int a = b - nfin;
+  const int g = a % ng, rb = a / ng;
+  const int j = threadIdx.x % CPS;
+  const int64_t r = (int64_t)rb * RPB + threadIdx.x / CPS;
+  const bool ok = r < M;
+  const int c0 = g * kFinGroup + j * E;
+  const int64_t off = r * C + c0;
+  float v[E], rv[E];
+  if (ok) {
+    load_vec(y + off, v);
+    if (res) load_vec(res + off, rv);
+  }
+  // wait for the finalize workgroups of channels [64 g, 64 g + 64)
+  constexpr int FPG = L == 64 ? kFinGroup / 4 : kFinGroup;   // finalize workgroups per group
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const int f = g * FPG + lane;
+    bool ready = false;
+    int it = 0;
+    for (; it < (e64 < 0 ? 0 : kFinSpins); ++it) {   // (a negative epoch: the fallback, for the tests)
+      const bool mine = lane >= FPG || f >= nfin || p6::ld_sc1(flags, f) == ep;
+      if (__all(mine)) { ready = true; break; }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (lane == 0) fb = ready ? 0 : 1;
+  }
+  __syncthreads();
+  float sc[E], sh[E];
+  if (fb) {
+    fin_fallback<L>(d, rows, M, g * kFinGroup, csc, csh);
+#pragma unroll
+    for (int e = 0; e < E; ++e) { sc[e] = csc[j * E + e]; sh[e] = csh[j * E + e]; }
+  } else {
+#pragma unroll
+    for (int e4 = 0; e4 < E; e4 += 4) {
+      const f32x4 a4 = p6::ld_sc1_x4(d.scale, c0 + e4), b4 = p6::ld_sc1_x4(d.shift, c0 + e4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { sc[e4 + k] = a4[k]; sh[e4 + k] = b4[k]; }
+    }
+  }
+  if (!ok) return;
+  // bn_act_kernel's arithmetic, term for term
+#pragma unroll
+  for (int e = 0; e < E; ++e) v[e] = fmaf(v[e], sc[e], sh[e]);
+  if (res) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] += rv[e];
+  }
+  if (relu) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] = fmaxf(v[e], 0.f);
+  }
+  store_vec(out + off, v);
+  if (mbits) {
+    unsigned bits = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) bits |= (p6::to_f(p6::from_f<T>(v[e])) > 0.f ? 1u : 0u) << e;
+    mbits[off / E] = (uint8_t)bits;
   }
 }
 
@@ -599,6 +746,41 @@ extern "C" int pose6d_bn_act_fwd_mask(int32_t dtype, const void* y, const float*
     bn_act_kernel<float><<<grid_for(M * C / 4), kThreads, 0, s>>>((const float*)y, scale, shift, (const float*)res,
                                                                     res_scale, res_shift, relu, (float*)out, M, C,
                                                                     relu_mask);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+// ready flags one pose6d_bn_finalize_act launch needs (int32, zeroed once by the caller)
+extern "C" int32_t pose6d_bn_finalize_act_flags(int32_t rows, int32_t C) {
+  return rows > 512 ? C : (C + 3) / 4;
+}
+
+extern "C" int pose6d_bn_finalize_act(int32_t dtype, const pose6d_bn_stats_t* bn, int32_t rows, int64_t count,
+                                      const void* y, const void* res, int32_t relu, void* out, uint8_t* relu_mask,
+                                      int32_t* flags, const int64_t* epoch, void* stream) {
+  P6_CHECK_ARG(bn && bn->C > 0 && bn->C % kFinGroup == 0 && rows > 0 && count > 0 &&
+                   rows == p6::ceil_div(count, (int64_t)32),
+               "pose6d_bn_finalize_act: bad sizes (C a multiple of 64, rows = ceil(count / 32))");
+  P6_CHECK_ARG(bn->partial && bn->gamma && bn->beta && bn->running_mean && bn->running_var && bn->scale && bn->shift &&
+                   bn->save_mean && bn->save_invstd && y && out && flags && epoch,
+               "pose6d_bn_finalize_act: null argument");
+  hipStream_t s = p6::stream_of(stream);
+  const int C = bn->C;
+  const int nfin = pose6d_bn_finalize_act_flags(rows, C);
+  auto go = [&](auto* typed) {
+    using TT = std::remove_pointer_t<decltype(typed)>;
+    constexpr int RPB = kThreads / (kFinGroup / V<TT>::E);
+    const int64_t napp = (int64_t)(C / kFinGroup) * p6::ceil_div(count, RPB);
+    const unsigned grid = (unsigned)(nfin + napp);
+    if (rows > 512)
+      bn_fin_act_kernel<TT, 256><<<grid, kThreads, 0, s>>>(*bn, rows, count, nfin, (const TT*)y, (const TT*)res, relu,
+                                                           (TT*)out, relu_mask, flags, epoch);
+    else
+      bn_fin_act_kernel<TT, 64><<<grid, kThreads, 0, s>>>(*bn, rows, count, nfin, (const TT*)y, (const TT*)res, relu,
+                                                          (TT*)out, relu_mask, flags, epoch);
+  };
+  if (dtype == POSE6D_DT_BF16) go((bf16*)nullptr);
+  else go((float*)nullptr);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
 }

@@ -263,6 +263,15 @@ class TrunkEngine:
                     ws_bn = max(ws_bn, 2 * (query("bn_bwd_workspace_rows", B * o.H * o.W) * 2 + 3) * o.C)
             elif isinstance(op, _PoolOp):
                 op.argmax = torch.empty(B, o.H, o.W, o.C, device=device, dtype=torch.uint8)
+        # training BN finalize + apply as one launch (pose6d_bn_finalize_act) where the form
+        # allows it: ready flags per BN (zeroed once) and one epoch counter per engine
+        self.bn_epoch = torch.zeros(1, device=device, dtype=torch.int64)
+        for op in self.ops:
+            if isinstance(op, _ActOp):
+                op.fin_flags = None
+                if self._fin_act_ok(op):
+                    n = query("bn_finalize_act_flags", op.cop.stats_rows, op.cop.cout)
+                    op.fin_flags = torch.zeros(max(n, 1), device=device, dtype=torch.int32)
         self._plan_bn_reduce(B, f32)
         ws_bn = max(ws_bn, 6 * max(op.cout for op in self.convs))   # pose6d_bn_bwd_partials' coefficients
         self.ws_wgrad = f32(max(ws_w // 4, 1))
@@ -280,6 +289,12 @@ class TrunkEngine:
         self._desc_dev = None
         self._pack_key = None
         self._build_pack_table()
+
+    @staticmethod
+    def _fin_act_ok(op):
+        """pose6d_bn_finalize_act's forms: a BN + (ReLU) + identity / no residual that is
+        stored (not applied inside a max pool), channels a multiple of 64."""
+        return not op.pooled and op.res_conv is None and op.cop.cout % 64 == 0
 
     def _plan_bn_reduce(self, B, f32):
         """A conv whose input is a BN + ReLU output that no other conv reads (each
@@ -396,6 +411,9 @@ class TrunkEngine:
             dual = self._dual_pairs()
         # training: a downsampling block's two BN finalizes (bn3, downsample BN: same
         # output grid) as one launch after conv3 (pose6d_bn_finalize_dual)
+        fused_fin = training and not fold and self.bn_fused_finalize_act
+        if fused_fin:
+            self.bn_epoch.add_(1)   # a fresh epoch for this forward's finalize -> apply hand-offs
         fin2 = {}
         if training and not fold and self.bn_dual_finalize:
             pos = {id(o): i for i, o in enumerate(self.ops)}
@@ -440,6 +458,8 @@ class TrunkEngine:
                      self.ws_sk_bytes, st)
                 if fold:
                     pass
+                elif fused_fin and a is not None and getattr(a, "fin_flags", None) is not None:
+                    pass   # finalized inside its BN's apply launch (pose6d_bn_finalize_act)
                 elif op in fin2:
                     r = fin2[op]
                     if r is not None:   # conv3: both BNs now; the downsample BN's finalize waited for it
@@ -454,6 +474,12 @@ class TrunkEngine:
                 c = op.cop
                 M = B * c.Ho * c.Wo
                 mb = op.mbits if training else None
+                if fused_fin and op.fin_flags is not None:
+                    st_ = _bn_stats(c)
+                    call("bn_finalize_act", dt, ctypes.addressof(st_), c.stats_rows, M, c.out.t,
+                         op.res_act.t if op.res_act else None, int(op.relu), op.out.t, mb, op.fin_flags,
+                         self.bn_epoch, st)
+                    continue
                 if op.res_conv is not None:
                     r = op.res_conv
                     call("bn_act_fwd_mask", dt, c.out.t, c.scale, c.shift, r.out.t, r.scale, r.shift, int(op.relu),
@@ -687,6 +713,11 @@ class TrunkEngine:
     # training forward: a downsampling block's two BN finalizes in one launch
     # (bit-identical to two pose6d_bn_finalize calls; attribute for the tests)
     bn_dual_finalize = True
+    # training forward: each other BN's finalize + apply in one launch (pose6d_bn_finalize_act;
+    # bit-identical to the two launches).  Off: measured slower -- the apply workgroups'
+    # flag poll + write-through parameter reads cost more than the launch boundary they
+    # remove (bf16 step 4.57 -> 4.70 ms, fp32 11.76 -> 11.89; profiles/r06_bn_finalize_act.txt)
+    bn_fused_finalize_act = False
     # training backward: a BN + ReLU whose output gradient one data-gradient launch
     # completes gets its reduce pass from that launch's epilogue (attribute for the tests)
     bwd_conv_bn_reduce = True

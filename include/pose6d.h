@@ -449,6 +449,22 @@ int pose6d_bn_act_fwd(int32_t dtype, const void *y, const float *scale, const fl
 int pose6d_bn_act_fwd_mask(int32_t dtype, const void *y, const float *scale, const float *shift, const void *res,
                            const float *res_scale, const float *res_shift, int32_t relu, void *out, uint8_t *relu_mask,
                            int64_t M, int32_t C, void *stream);
+/* Training BatchNorm finalize + apply in ONE launch: pose6d_bn_finalize(bn, training = 1)
+ * followed by pose6d_bn_act_fwd_mask(y, bn->scale, bn->shift, res, NULL, NULL, relu, out,
+ * relu_mask), bit for bit (the identity-residual / no-residual forms; C a multiple of 64,
+ * rows = ceil(count / 32) as the conv epilogue wrote them).  The apply workgroups wait for
+ * the finalize workgroups of their channels through `flags` (pose6d_bn_finalize_act_flags
+ * int32, zeroed ONCE by the caller, then left to the launches) and `epoch`, a device
+ * int64 the caller advances (+1) between two launches on the same flags and never
+ * changes while one runs; an apply workgroup that does not see its flags in time
+ * computes its channels itself (same arithmetic), so nothing depends on dispatch order
+ * (a NEGATIVE epoch sends every apply workgroup that way at once: tests).
+ * Replaces pose6d_bn_finalize + pose6d_bn_act_fwd_mask of the trunk's training forward
+ * (bn_stats_finalize / bn_act, BatchNorm2d + ReLU [+ residual] of every Bottleneck). */
+int32_t pose6d_bn_finalize_act_flags(int32_t rows, int32_t C);
+int pose6d_bn_finalize_act(int32_t dtype, const pose6d_bn_stats_t *bn, int32_t rows, int64_t count, const void *y,
+                           const void *res, int32_t relu, void *out, uint8_t *relu_mask, int32_t *flags,
+                           const int64_t *epoch, void *stream);
 /* backward of bn_act_fwd for one BN: dz = dout * mask, mask = out > 0 when `out` is
  * given, else (relu_scale/relu_shift given: a ReLU BN without residual) the sign
  * bn_act_fwd stored, recomputed from y as round(y * relu_scale + relu_shift) > 0

@@ -282,3 +282,93 @@ def test_trunk_backward_conv_bn_reduce():
     med = lambda e: e[len(e) // 2]
     assert med(e_fold) <= 1.25 * med(e_unf) + 1e-3, (med(e_fold), med(e_unf))
     assert e_fold[-1] <= 1.5 * e_unf[-1] + 1e-2, (e_fold[-1], e_unf[-1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_trunk_finalize_act_one_launch_is_bit_identical(dtype):
+    """pose6d_bn_finalize_act (the training BN finalize + apply as one launch, the apply
+    workgroups waiting on the finalize workgroups' ready flags) against the two launches
+    it replaces (pose6d_bn_finalize + pose6d_bn_act_fwd_mask): every activation, ReLU
+    mask, batch statistic, running statistic and the features bit for bit, over three
+    training forwards (epochs advance), at batch 8 (rows <= 512: the one-wave fold) and
+    batch 32 (layer1/2: rows > 512, the workgroup fold)."""
+    import copy
+    from models.pose_net_rgbd_geometric import PoseNetRGBDGeometric
+    from pose6d.trunk import TrunkEngine, _ActOp, _ConvOp
+    torch.manual_seed(0)
+    m0 = PoseNetRGBDGeometric(pretrained=False).train()
+    engs = []
+    for fused in (True, False):
+        m = copy.deepcopy(m0).cuda()
+        e = TrunkEngine(m.backbone, 3)
+        e.set_dtype(dtype)
+        e.bn_fused_finalize_act = fused
+        engs.append((m, e))
+    for B in (8, 32):
+        for it in range(3):
+            x = torch.randn(B, 3, 64 if B == 32 else 96, 64 if B == 32 else 96,
+                            generator=torch.Generator().manual_seed(10 * B + it)).cuda()
+            feats = [e.forward(x, True).clone() for _, e in engs]
+            torch.cuda.synchronize()
+            assert torch.equal(feats[0], feats[1]), (B, it)
+            a, b = engs[0][1], engs[1][1]
+            assert sum(op.fin_flags is not None for op in a.ops if isinstance(op, _ActOp)) >= 40
+            for oa, ob in zip(a.ops, b.ops):
+                if not (isinstance(oa, _ActOp) and oa.pooled):   # (a pooled activation is never stored)
+                    assert torch.equal(oa.out.t, ob.out.t), oa.out.name
+                if isinstance(oa, _ActOp) and oa.mbits is not None:
+                    assert torch.equal(oa.mbits, ob.mbits), oa.out.name
+                if isinstance(oa, _ConvOp):
+                    for f in ("scale", "shift", "mean", "inv"):
+                        assert torch.equal(getattr(oa, f), getattr(ob, f)), (oa.out.name, f)
+            for (ka, va), (kb, vb) in zip(engs[0][0].state_dict().items(), engs[1][0].state_dict().items()):
+                assert torch.equal(va, vb), ka
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows_case", ["wave_fold", "block_fold"])
+def test_bn_finalize_act_fallback_is_bit_identical(rows_case):
+    """The apply workgroups' own fold (taken when the finalize's ready flags do not arrive
+    in time; forced here with a negative epoch) gives the finalize's scale / shift bits:
+    the fused launch's outputs equal the two-launch path's."""
+    import ctypes
+    from pose6d._lib import DT_BF16, call, stream
+    from pose6d.trunk import _BnStats
+    torch.manual_seed(1)
+    dev = "cuda"
+    M = 6272 if rows_case == "wave_fold" else 25088   # rows 196 (<= 512) / 784
+    C = 256
+    rows = (M + 31) // 32
+    y = (torch.randn(M, C, device=dev) * 2 + 0.3).bfloat16()
+    yf = y.float()
+    part = torch.zeros(2, C, rows, device=dev)
+    for r in range(rows):   # the conv epilogue's (sum, M2 about the block mean) per 32 rows
+        blk = yf[32 * r:32 * r + 32]
+        part[0, :, r] = blk.sum(0)
+        part[1, :, r] = ((blk - blk.mean(0)) ** 2).sum(0)
+    res = torch.randn(M, C, device=dev).bfloat16()
+    outs = []
+    g0, b0 = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
+    for mode in ("separate", "fallback"):
+        gamma, beta = g0.clone(), b0.clone()
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        nbt = torch.zeros(1, device=dev, dtype=torch.int64)
+        sc, sh, mu, inv = (torch.empty(C, device=dev) for _ in range(4))
+        st = _BnStats(part.data_ptr(), gamma.data_ptr(), beta.data_ptr(), rm.data_ptr(), rv.data_ptr(),
+                      nbt.data_ptr(), sc.data_ptr(), sh.data_ptr(), mu.data_ptr(), inv.data_ptr(), 0.1, 1e-5, C)
+        out = torch.empty_like(y)
+        mb = torch.empty(M * C // 8, device=dev, dtype=torch.uint8)
+        if mode == "separate":
+            call("bn_finalize", part, rows, C, M, gamma, beta, rm, rv, nbt, 0.1, 1e-5, 1, sc, sh, mu, inv, None,
+                 stream())
+            call("bn_act_fwd_mask", DT_BF16, y, sc, sh, res, None, None, 1, out, mb, M, C, stream())
+        else:
+            flags = torch.zeros(4096, device=dev, dtype=torch.int32)
+            epoch = torch.full((1,), -5, device=dev, dtype=torch.int64)
+            call("bn_finalize_act", DT_BF16, ctypes.addressof(st), rows, M, y, res, 1, out, mb, flags, epoch,
+                 stream())
+        torch.cuda.synchronize()
+        outs.append((out, mb, sc, sh, mu, inv, rm, rv, nbt))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
