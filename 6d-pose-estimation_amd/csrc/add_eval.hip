@@ -20,6 +20,10 @@
 // whenever sqrtf(new) == sqrtf(old) (same sqrt value => the old, earlier j wins).
 #include "common.h"
 
+#ifndef POSE6D_ADD_HIT
+#define POSE6D_ADD_HIT 1   // build-time: 0 = timing-only build, the minimum updates skipped (wrong results)
+#endif
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -149,19 +153,25 @@ __global__ __launch_bounds__(kThreads) void add_points_kernel(
 #pragma unroll
         for (int i = 0; i < PPT; ++i) s[u][i] = sqdist(qx[i], qy[i], qz[i], g[u]);
       // min over the trip first (v_min3), one compare per point: any s < best <=> min(s) < best
+      float m[PPT];
 #pragma unroll
       for (int i = 0; i < PPT; ++i) {
-        float m = s[0][i];
+        m[i] = s[0][i];
 #pragma unroll
-        for (int u = 1; u < U; ++u) m = __builtin_fminf(m, s[u][i]);
-        hit |= __ballot(m < best[i]);
+        for (int u = 1; u < U; ++u) m[i] = __builtin_fminf(m[i], s[u][i]);
+        hit |= __ballot(m[i] < best[i]);
       }
+#if POSE6D_ADD_HIT == 0
+      (void)m;   // timing-only build: the updates skipped (wrong results)
+      if (hit == 0x1234567ull) best[0] = 0.f;
+#else
       if (__builtin_expect(hit != 0, 0)) {
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
           for (int i = 0; i < PPT; ++i) update(i, s[u][i], j0 + jj + u);
       }
+#endif
     }
     for (; jj < jn; ++jj) {
       const float4 g = gs[jj];

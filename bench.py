@@ -30,10 +30,10 @@ PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0       # HBM3E spec
 FWD_BYTES_PER_CROP = 58.45e6   # bf16 fused-ideal forward bytes / crop
 FWD_BYTES_PER_CROP_F32 = 116.89e6   # the same forward in fp32
-PEAK_F32_VALU_TFLOPS = 157.3   # MI355X fp32 vector peak (counts packed v_pk_fma_f32 as 2)
-# the rate a kernel issuing unpacked fp32 VALU (v_fma_f32 / v_sub_f32 ...) can reach: half the
-# packed figure (the ADD kernel is unpacked: the packed form measured slower)
-PEAK_F32_VALU_UNPACKED_TFLOPS = PEAK_F32_VALU_TFLOPS / 2
+# MI355X fp32 vector peak: 64 flop/clk/SIMD, reached by unpacked v_fma_f32
+# (a wave64 instruction every 2 cycles on a SIMD-32) and by v_pk_fma_f32 alike
+# (MI355X_MICROARCH.md constants table)
+PEAK_F32_VALU_TFLOPS = 157.3
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X fp32 MFMA peak = the vector rate (MI355X_MICROARCH.md)
 # PoseNetRGB forward FLOPs per crop: ResNet50 trunk 8.175 G + the two
 # 2048-2048-1024-512-{4,3} heads (13.64 M multiply-adds)
@@ -538,11 +538,9 @@ def add_eval_throughput(dev, B=256, N=2000, reps=10, cpu=True):
             "value": round(B / t, 1), "unit": "samples/s", "ms_per_batch": round(t * 1e3, 4), "dtype": "f32",
             "pairs_per_s": round(pairs / t, 1), "add_01d_acc": round(float(m["add_01d_acc"]), 3),
             "valu_roofline": {"achieved": round(pairs * ADD_FLOPS_PER_PAIR / t / 1e12, 2),
-                              "peak": PEAK_F32_VALU_TFLOPS, "peak_kind": "fp32 vector peak (packed v_pk_fma_f32)",
+                              "peak": PEAK_F32_VALU_TFLOPS, "peak_kind": "fp32 vector peak (v_fma_f32 / v_pk_fma_f32)",
                               "unit": "TFLOP/s",
-                              "frac": round(pairs * ADD_FLOPS_PER_PAIR / t / 1e12 / PEAK_F32_VALU_TFLOPS, 4),
-                              "frac_of_unpacked_rate": round(
-                                  pairs * ADD_FLOPS_PER_PAIR / t / 1e12 / PEAK_F32_VALU_UNPACKED_TFLOPS, 4)}}
+                              "frac": round(pairs * ADD_FLOPS_PER_PAIR / t / 1e12 / PEAK_F32_VALU_TFLOPS, 4)}}
 
 
 def crop_throughput(dev, B=32, reps=20):
