@@ -47,16 +47,21 @@ def test_ddp_bucketed_step_matches_mean_gradient_update(world, batch, bucket_mb)
 
 
 @pytest.mark.gpu
-def test_bench_world2_json_line():
+@pytest.mark.parametrize("profile", [False, True], ids=["plain", "with-roofline"])
+def test_bench_world2_json_line(profile):
     """bench.py's N > 1 path end to end (configs[4] per rank: bs32, 25 MB buckets,
     segmented graphs), 2 ranks sharing the box's one GPU over gloo
     (POSE6D_BENCH_SHARE_GPU=1; RCCL needs a GPU per rank): the JSON line reports the
-    whole job -- n_gpus 2, global batch 64, value = 64 crops x steps / max-over-ranks time."""
+    whole job -- n_gpus 2, global batch 64, value = 64 crops x steps / max-over-ranks time.
+    with-roofline: rank 0 also runs the in-step roofline capture after the timed loop
+    (the line an 8-GPU run prints), while rank 1 leaves."""
     import json
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", POSE6D_BENCH_SHARE_GPU="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr", "127.0.0.1", "--master-port", "29671", os.path.join(REPO, "bench.py"), "--gpus", "2",
-           "--steps", "3", "--warmup", "1", "--no-side", "--no-fp32", "--no-cpu-baseline", "--no-kernel-profile"]
+           "--master-addr", "127.0.0.1", "--master-port", str(29671 + int(profile)), os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--no-side", "--no-fp32", "--no-cpu-baseline"]
+    if not profile:
+        cmd.append("--no-kernel-profile")
     r = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, _report(r)
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -65,6 +70,9 @@ def test_bench_world2_json_line():
     assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 64 and res["config"]["per_gpu_batch"] == 32
     assert res["config"]["parallelism"] == "dp2" and res["scaling"] == "weak"
     assert res["value"] > 0 and abs(res["value"] - 64 * 1e3 / res["ms_per_step"]) < 1e-3 * res["value"] + 0.1
+    if profile:
+        assert res["roofline"].get("kernel", "").startswith("conv_bwd"), res["roofline"]
+        assert res["roofline"]["frac"] > 0 and res["breakdown"]["kernels_per_step"] > 100
 
 
 @pytest.mark.gpu
