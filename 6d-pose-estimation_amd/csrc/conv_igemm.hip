@@ -1275,7 +1275,9 @@ __global__ __launch_bounds__(64 * NW) void conv_lds_kernel(const T* __restrict__
 #define POSE6D_BWD_F32_MS 32   // build-time (A/B): pixels per fp32 weight-gradient stage in the fused launch
 #endif
 constexpr int kBwdF32MS = POSE6D_BWD_F32_MS;
-template <int DMODE, int DS, int WS, typename T = bf16>
+// WBT (fp32 only): the weight-gradient tile, 64 or 128 (the wider KxK convs' plans: 128x128
+// on 32-pixel stages, conv_wgrad_lds_body_f32)
+template <int DMODE, int DS, int WS, typename T = bf16, int WBT = 64>
 __global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ wt,
                                                             const T* __restrict__ dres, T* __restrict__ dx,
                                                             Geom gd, int nd, int nd_pad, int wfirst,
@@ -1294,6 +1296,8 @@ __global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const T* __restrict_
     // kGemm data gradient <=> pointwise conv: the weight gradient takes the pointwise body
     if constexpr (sizeof(T) == 2)
       conv_wgrad_lds_body<64, 64, WS, DMODE == kGemm>(smem, b - w0, x, dy, ws, gw);
+    else if constexpr (WBT == 128)
+      conv_wgrad_lds_body_f32<32, WS, DMODE == kGemm, 128>(smem, b - w0, x, dy, ws, gw);
     else
       conv_wgrad_lds_body_f32<kBwdF32MS, WS, DMODE == kGemm>(smem, b - w0, x, dy, ws, gw);
   } else if (b >= r0) {
@@ -1986,7 +1990,7 @@ extern "C" int pose6d_conv2d_dgrad_tuned(int32_t dtype, const void* dy, const vo
 
 namespace {
 
-template <int DMODE, int DS, int WS, typename T = bf16>
+template <int DMODE, int DS, int WS, typename T = bf16, int WBT = 64>
 int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void* wt, const void* dres, void* dx,
                const void* x, float* ws, const ReduceJob& rj, hipStream_t s, int order) {
   Geom gd = gd0;
@@ -1999,9 +2003,11 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
   const int nk = fast_nk(DMODE, gd, LK<T>::KS);
   const int ring_d = (nk < DS ? (nk > 0 ? nk : 1) : DS) * 128 * 128;
   const int epi = 64 * (64 * (int)sizeof(T) + 16) + (gd.bnr_part ? bnr_lds(4, 64) : 0);
-  const int ring_w = sizeof(T) == 2 ? WS * 128 * 128 : WS * WgF32<kBwdF32MS>::STAGE;
+  const int ring_w = sizeof(T) == 2 ? WS * 128 * 128
+                                    : (WBT == 128 ? WS * WgF32<32, 128>::STAGE : WS * WgF32<kBwdF32MS>::STAGE);
   int lds = ring_d > epi ? ring_d : epi;
   lds = lds > ring_w ? lds : ring_w;
+  if (sizeof(T) == 4 && WBT == 128 && lds < acc_stage_bytes<128, 128>()) lds = acc_stage_bytes<128, 128>();
   // longest workgroups first: the weight gradient's K-steps per split against the
   // data gradient's K-steps per tile.  fp32: a 64-pixel weight-gradient stage is twice
   // the MACs of a 32-channel data-gradient K-step (28x28 128->512 fp32: 79.5 -> 72.5 us
@@ -2016,7 +2022,7 @@ int launch_bwd(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void*
   const int wfirst = order >= 0 ? order
                                 : (POSE6D_BWD_ORDER == 2 || (POSE6D_BWD_ORDER && WSTEP * p6::ceil_div(gw.mps, 64) >= nk));
   const int grid = wfirst ? ((nw + 7) & ~7) + nd + rj.nblk : nd_pad + nw + rj.nblk;
-  conv_bwd_kernel<DMODE, DS, WS, T><<<grid, kThreads, lds, s>>>(
+  conv_bwd_kernel<DMODE, DS, WS, T, WBT><<<grid, kThreads, lds, s>>>(
       (const T*)dy, (const T*)wt, (const T*)dres, (T*)dx, gd, nd, nd_pad, wfirst, (const T*)x, ws, gw, rj);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
@@ -2078,7 +2084,12 @@ int fused_ds(int dtype, int stages) {
 template <int DMODE>
 int launch_bwd_mode(int dtype, int ds, const Geom& gd, const p6::WGeom& gw, const void* dy, const void* wt,
                     const void* dres, void* dx, const void* x, float* ws, const ReduceJob& rj, hipStream_t s,
-                    int order) {
+                    int order, int wbt = 64) {
+  if (dtype == POSE6D_DT_F32 && wbt == 128)
+    return fused_ds(dtype, ds) == 2
+               ? launch_bwd<DMODE, 2, POSE6D_WGRAD_STAGES_F32, float, 128>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order)
+               : launch_bwd<DMODE, 3, POSE6D_WGRAD_STAGES_F32, float, 128>(gd, gw, dy, wt, dres, dx, x, ws, rj, s,
+                                                                          order);
   if (dtype == POSE6D_DT_F32)
     return fused_ds(dtype, ds) == 2
                ? launch_bwd<DMODE, 2, POSE6D_WGRAD_STAGES_F32, float>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order)
@@ -2096,21 +2107,25 @@ int launch_bwd_mode(int dtype, int ds, const Geom& gd, const p6::WGeom& gw, cons
 // otherwise as the separate pose6d_conv2d_dgrad + pose6d_conv2d_wgrad launches.
 // dx == NULL: weight gradient only.
 namespace {
+#ifndef POSE6D_BWD_F32_FUSE128
+#define POSE6D_BWD_F32_FUSE128 1   // build-time (A/B): 0 = the fp32 128x128 weight gradients as launches of their own
+#endif
 bool bwd_fused(int dtype, const Plan& pd, const p6::WgradPlan& pw, const pose6d_tuning_t* tn) {
   // the fused kernels carry the 64x64 weight-gradient bodies (conv_bwd_kernel) and the
   // bf16 128x128 one (conv_bwd8_kernel: its data gradient on 128x64 tiles of 8 waves)
   if (!pd.fast || pd.tile != 3 || !(pd.stages == 2 || pd.stages == 4) || !pw.fast) return false;
   if (tune(tn, &pose6d_tuning_t::bwd_separate, 0) != 0) return false;
-  if (pw.bm == 128) return dtype == POSE6D_DT_BF16 && (pw.stages == 2 || pw.stages == 3);
+  if (pw.bm == 128 && dtype == POSE6D_DT_BF16) return pw.stages == 2 || pw.stages == 3;
+  if (pw.bm == 128) return POSE6D_BWD_F32_FUSE128 && pw.stages == POSE6D_WGRAD_STAGES_F32;   // fp32 KxK, 128x128
   return pw.bm == 64 && pw.stages == (dtype == POSE6D_DT_BF16 ? POSE6D_WGRAD_STAGES : POSE6D_WGRAD_STAGES_F32);
 }
 
-// the data-gradient plan a fused launch runs: the 8-wave launch (128x128 weight-gradient
-// tiles) takes 128x64 data-gradient tiles of 8 waves (tile 5), which also sets the
-// BatchNorm-reduce partial rows (bnr_plan_rows)
-Plan fused_dplan(const Plan& pd, const p6::WgradPlan& pw) {
+// the data-gradient plan a fused launch runs: the bf16 8-wave launch (128x128 weight-
+// gradient tiles) takes 128x64 data-gradient tiles of 8 waves (tile 5), which also sets
+// the BatchNorm-reduce partial rows (bnr_plan_rows); the fp32 launch keeps the plan's tile
+Plan fused_dplan(int dtype, const Plan& pd, const p6::WgradPlan& pw) {
   Plan q = pd;
-  if (pw.bm == 128) q.tile = 5;
+  if (dtype == POSE6D_DT_BF16 && pw.bm == 128) q.tile = 5;
   return q;
 }
 
@@ -2193,7 +2208,7 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
                "pose6d_conv2d_backward: workspace %lld bytes < %lld needed", (long long)ws_bytes,
                (long long)pw.splits * Cout * gw.Kpad * 4);
   hipStream_t s = p6::stream_of(stream);
-  int rc = check_bnr(bnr, fused_dplan(pd, pw), dres, dx);
+  int rc = check_bnr(bnr, fused_dplan(dtype, pd, pw), dres, dx);
   if (rc) return rc;
   Geom gd = pd.g;
   set_bnr(gd, bnr);
@@ -2208,7 +2223,7 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
   const bool direct = POSE6D_WGRAD_DIRECT && gw.splits == 1 && KH == 1 && KW == 1 && gw.Kpad == Cin &&
                       Cin_real == Cin && !accumulate;
   float* slab = direct ? dw : workspace;
-  if ((phases & 1) && pw.bm == 128) {
+  if ((phases & 1) && pw.bm == 128 && dtype == POSE6D_DT_BF16) {
     switch (pd.mode) {
       case kGemm:
         rc = launch_bwd8_mode<kGemm>(pd.stages, pw.stages, gd, gw, dy, wt, dres, dx, x, slab, carried, s, order);
@@ -2223,13 +2238,14 @@ int conv_backward_impl(int32_t dtype, const void* x, const void* dy, const void*
   } else if (phases & 1) {
     switch (pd.mode) {
       case kGemm:
-        rc = launch_bwd_mode<kGemm>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, slab, carried, s, order);
+        rc = launch_bwd_mode<kGemm>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, slab, carried, s, order, pw.bm);
         break;
       case kDgradS2:
-        rc = launch_bwd_mode<kDgradS2>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, slab, carried, s, order);
+        rc = launch_bwd_mode<kDgradS2>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, slab, carried, s, order,
+                                       pw.bm);
         break;
       default:
-        rc = launch_bwd_mode<kDgrad>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, slab, carried, s, order);
+        rc = launch_bwd_mode<kDgrad>(dtype, pd.stages, gd, gw, dy, wt, dres, dx, x, slab, carried, s, order, pw.bm);
         break;
     }
   }
@@ -2395,7 +2411,7 @@ extern "C" int pose6d_conv2d_backward_bn_rows(int32_t dtype, int32_t N, int32_t 
   const Plan pd = choose(dtype, mode, gd0, true);
   p6::WgradPlan pw;
   p6::wgrad_geom(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, &pw);
-  return bnr_plan_rows(bwd_fused(dtype, pd, pw, nullptr) ? fused_dplan(pd, pw) : choose(dtype, mode, gd0, false));
+  return bnr_plan_rows(bwd_fused(dtype, pd, pw, nullptr) ? fused_dplan(dtype, pd, pw) : choose(dtype, mode, gd0, false));
 }
 
 extern "C" int pose6d_conv2d_backward_chain_bn(int32_t dtype, const void* x, const void* dy, const void* wt,
