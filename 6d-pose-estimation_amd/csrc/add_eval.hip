@@ -9,7 +9,12 @@
 //                      transformed ground-truth mesh through LDS in 2048-point tiles
 //                      (broadcast reads, no bank conflicts) and keeps a running
 //                      nearest-point minimum per predicted point in registers: 4 gt
-//                      points per trip, one scalar branch per trip (round 6).
+//                      points per trip, one scalar branch per trip (round 6).  The
+//                      minimum starts from the point's own ground-truth point and a
+//                      two-hop walk on the mesh's model-space neighbour table
+//                      (add_neighbors_kernel, built once per mesh table), so the sweep
+//                      almost never takes its update branch; the first-index tie rule
+//                      is order-free, so the bits do not depend on the seeds.
 //   add_reduce_kernel  grid B: fixed-order fp64 means (deterministic), 0.1d test.
 //
 // Bit-exactness contract (pinned by tests/golden/add_loss.npz):
@@ -22,6 +27,12 @@
 
 #ifndef POSE6D_ADD_HIT
 #define POSE6D_ADD_HIT 1   // build-time: 0 = timing-only build, the minimum updates skipped (wrong results)
+#endif
+#ifndef POSE6D_ADD_SEED
+#define POSE6D_ADD_SEED 1  // build-time: 1 = every point's minimum starts at its own ground-truth point
+#endif
+#ifndef POSE6D_ADD_HOPS
+#define POSE6D_ADD_HOPS 2  // build-time: neighbour-table hops of the seed walk (1 = the point's own row only)
 #endif
 
 namespace {
@@ -79,16 +90,17 @@ __device__ __forceinline__ float sqdist(float ax, float ay, float az, float4 g) 
 // squared distances of a trip are independent chains (3 sub, mul, 2 fma each), and
 // ONE compare-and-branch per trip asks whether any of them beat its running minimum
 // -- after the first few hundred ground-truth points almost never -- instead of a
-// branch per (point, gt point).  The rare update replays the trip's candidates in
-// ground-truth order, so every point sees its j's in the same order as the plain
-// loop: the first-index tie rule is unchanged.
+// branch per (point, gt point).  The rare update replays the trip's candidates
+// through `update`, whose first-index tie rule does not depend on the visiting order
+// (the sweep starts from the point's own ground-truth point, POSE6D_ADD_SEED).
 template <int PPT, int U>
 __global__ __launch_bounds__(kThreads) void add_points_kernel(
     const float* __restrict__ pred_rot, const float* __restrict__ pred_trans,
     const float* __restrict__ gt_rot, const float* __restrict__ gt_trans,
     const int64_t* __restrict__ obj_ids, const float* __restrict__ points,
     const int32_t* __restrict__ off, const int32_t* __restrict__ npts, int n_slots, int max_npts,
-    float* __restrict__ min_dist, int32_t* __restrict__ argmin, float* __restrict__ pt_add) {
+    float* __restrict__ min_dist, int32_t* __restrict__ argmin, float* __restrict__ pt_add,
+    const uint16_t* __restrict__ nbr, int K) {
   constexpr int kPts = kThreads * PPT;
   __shared__ float4 gs[kTile];
   const int b = blockIdx.y;
@@ -104,7 +116,12 @@ __global__ __launch_bounds__(kThreads) void add_points_kernel(
   const float* P = points + 3 * (int64_t)off[oid];
   const int tid = threadIdx.x;
 
-  float qx[PPT], qy[PPT], qz[PPT], best[PPT];
+  // best = smallest squared distance seen, bi = the SMALLEST index among the seen
+  // candidates whose sqrtf equals sqrtf(best) (the reference's first-index argmin over
+  // the roots), thr = the largest squared distance that can still matter: a root equal
+  // to sqrtf(best) needs the two within 2^-20 relative (a correctly rounded sqrt of
+  // values farther apart differs by >= 8 ulps of the root), so thr = best (1 + 2^-19).
+  float qx[PPT], qy[PPT], qz[PPT], best[PPT], thr[PPT];
   int bi[PPT];
 #pragma unroll
   for (int i = 0; i < PPT; ++i) {
@@ -116,28 +133,101 @@ __global__ __launch_bounds__(kThreads) void add_points_kernel(
       const float4 q = xform(P + 3 * k, Rp, tp, n);
       qx[i] = q.x; qy[i] = q.y; qz[i] = q.z;
       const float4 g = xform(P + 3 * k, Rg, tg, n);
-      pt_add[(int64_t)b * max_npts + k] = sqrtf(sqdist(q.x, q.y, q.z, g));  // add_loss.py:182
+      const float skk = sqdist(q.x, q.y, q.z, g);
+      pt_add[(int64_t)b * max_npts + k] = sqrtf(skk);  // add_loss.py:182
+#if POSE6D_ADD_SEED
+      // seed: the point's own ground-truth point (the ADD pair, already at hand) -- for
+      // a pose near the truth it is near the nearest one, so the sweep below seldom
+      // finds a better candidate and its per-trip test almost never branches.  The
+      // sweep then sees j < k after k, which the order-free rule of `update` handles.
+      // (NaN distances never become a minimum, as in the sweep: `s < best` is false.)
+      if (skk == skk) { best[i] = skk; bi[i] = k; }
+#endif
     } else {
       best[i] = -__builtin_inff();   // idle lane: nothing beats it (its result is never stored)
     }
+    thr[i] = best[i] + best[i] * 0x1p-19f;
   }
 
-  // a new squared minimum keeps the old index iff sqrtf maps both to the same value;
-  // that needs them within a few ulps (a correctly rounded sqrt of values 2^-20 apart,
-  // relative, differs by >= 8 ulps of the root), so the two square roots are taken only
-  // then -- the common update is a subtract, a multiply and a compare
+  // order-free: the result is the same for any visiting order of the j's.  A new
+  // squared minimum keeps the old index (or takes j if smaller) iff sqrtf maps both to
+  // the same value, which needs them within 2^-20 relative, so the two square roots are
+  // taken only then -- the common update is a subtract, a multiply and a compare; a
+  // candidate in [best, thr] is a possible root tie and wins only with a smaller index
   auto update = [&](int i, float s, int j) {
     if (s < best[i]) {
       const float gap = best[i] - s;   // exact when the two are close (Sterbenz)
       if (!(gap <= best[i] * 0x1p-20f) || sqrtf(s) != sqrtf(best[i])) bi[i] = j;
+      else bi[i] = min(bi[i], j);
       best[i] = s;
+      thr[i] = s + s * 0x1p-19f;
+    } else if (j < bi[i] && s <= thr[i] && sqrtf(s) == sqrtf(best[i])) {
+      bi[i] = j;
     }
   };
+  bool tile_ready = false;   // the mesh's only tile already in LDS (seeded from it)
+#if POSE6D_ADD_SEED
+  // seeds, part 2: the point's K nearest mesh neighbours in model space
+  // (pose6d_add_neighbors, [point][K] local indices) -- the nearest transformed ground-
+  // truth point of a near-truth pose is almost always among them, so after these the
+  // sweep's per-trip test seldom fires.  Each seed is a genuine candidate (index
+  // clamped into the mesh, distance computed as the sweep computes it), so a poor or
+  // even wrong table costs time, never bits.
+  if (nbr != nullptr) {
+    if (n <= kTile) {
+      for (int jj = tid; jj < n; jj += kThreads) gs[jj] = xform(P + 3 * jj, Rg, tg, n);
+      __syncthreads();
+      tile_ready = true;
+    }
+    const uint16_t* nb = nbr + (int64_t)off[oid] * K;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int k = base + tid + kThreads * i;
+      if (k >= n) continue;
+      // a greedy walk on the neighbour graph: the row of the point's own index, then the
+      // row of the best candidate found so far while that keeps moving (the nearest
+      // transformed point sits near x = Rg^T (q - tg) in model space, a short walk from k)
+      int cur = k;
+      for (int h = 0; h < POSE6D_ADD_HOPS; ++h) {
+        const uint16_t* row = nb + (int64_t)cur * K;
+        for (int t = 0; t < K; t += 8) {
+          const uint4 w = *reinterpret_cast<const uint4*>(row + t);   // 8 indices (K % 8 == 0, 16-B rows)
+          const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+          float sv[8];
+          int jv[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int j = min((int)((ww[e >> 1] >> (16 * (e & 1))) & 0xffffu), n - 1);
+            const float4 g = tile_ready ? gs[j] : xform(P + 3 * j, Rg, tg, n);
+            sv[e] = sqdist(qx[i], qy[i], qz[i], g);
+            jv[e] = j;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) update(i, sv[e], jv[e]);
+        }
+        if (bi[i] == cur) break;   // nothing nearer around cur
+        cur = bi[i];
+      }
+    }
+  }
+  // the candidates of the best's own trip that precede it (<= U - 1 of them): the
+  // sweep's trip test only asks for strict improvements there (see below)
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    if (base + tid + kThreads * i >= n) continue;
+    for (int j = bi[i] & ~(U - 1); j < bi[i]; ++j) {
+      const float4 g = tile_ready ? gs[j] : xform(P + 3 * j, Rg, tg, n);
+      update(i, sqdist(qx[i], qy[i], qz[i], g), j);
+    }
+  }
+#endif
   for (int j0 = 0; j0 < n; j0 += kTile) {
     const int jn = min(kTile, n - j0);
-    __syncthreads();
-    for (int jj = tid; jj < jn; jj += kThreads) gs[jj] = xform(P + 3 * (j0 + jj), Rg, tg, n);
-    __syncthreads();
+    if (!tile_ready) {
+      __syncthreads();
+      for (int jj = tid; jj < jn; jj += kThreads) gs[jj] = xform(P + 3 * (j0 + jj), Rg, tg, n);
+      __syncthreads();
+    }
     int jj = 0;
     for (; jj + U <= jn; jj += U) {
       float s[U][PPT];
@@ -152,20 +242,35 @@ __global__ __launch_bounds__(kThreads) void add_points_kernel(
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int i = 0; i < PPT; ++i) s[u][i] = sqdist(qx[i], qy[i], qz[i], g[u]);
-      // min over the trip first (v_min3), one compare per point: any s < best <=> min(s) < best
+      // min over the trip first (v_min3), one compare per point: any s <= thr <=> min(s) <= thr
       float m[PPT];
 #pragma unroll
       for (int i = 0; i < PPT; ++i) {
         m[i] = s[0][i];
 #pragma unroll
         for (int u = 1; u < U; ++u) m[i] = __builtin_fminf(m[i], s[u][i]);
-        hit |= __ballot(m[i] < best[i]);
+        hit |= __ballot(m[i] <= thr[i]);
       }
 #if POSE6D_ADD_HIT == 0
       (void)m;   // timing-only build: the updates skipped (wrong results)
       if (hit == 0x1234567ull) best[0] = 0.f;
 #else
       if (__builtin_expect(hit != 0, 0)) {
+#if POSE6D_ADD_SEED
+        // most of these are a point meeting its own current best (m == best <= thr):
+        // only a trip wholly before the best's trip can hold a root tie that wins (a
+        // smaller index), so elsewhere only a strict improvement counts.  (The best's
+        // own trip, up to the best, was replayed when the best was taken -- by the
+        // sweep's replay below, or after the seed walk.)
+        uint64_t real = 0;
+        const int jb = j0 + jj;
+#pragma unroll
+        for (int i = 0; i < PPT; ++i)
+          real |= __ballot(m[i] < best[i] || (jb < (bi[i] & ~(U - 1)) && m[i] <= thr[i]));
+        hit = real;
+      }
+      if (hit != 0) {
+#endif
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -187,6 +292,44 @@ __global__ __launch_bounds__(kThreads) void add_points_kernel(
       if (argmin) argmin[(int64_t)b * max_npts + k] = bi[i];
     }
   }
+}
+
+// pose6d_add_neighbors: every mesh point's K nearest other points in model space
+// (plain fp32 distances -- the table only seeds add_points_kernel's search, it never
+// decides a result); one thread per point, a sorted K-list in registers, the mesh read
+// as broadcast loads.  A one-time setup per mesh table.
+template <int K>
+__global__ __launch_bounds__(kThreads) void add_neighbors_kernel(const float* __restrict__ points,
+                                                                 const int32_t* __restrict__ off,
+                                                                 const int32_t* __restrict__ npts,
+                                                                 uint16_t* __restrict__ nbr) {
+  const int oid = blockIdx.y;
+  const int n = npts[oid];
+  const int k = blockIdx.x * kThreads + threadIdx.x;
+  if (k >= n) return;
+  const float* P = points + 3 * (int64_t)off[oid];
+  const float px = P[3 * k], py = P[3 * k + 1], pz = P[3 * k + 2];
+  float d[K];
+  int id[K];
+#pragma unroll
+  for (int t = 0; t < K; ++t) { d[t] = __builtin_inff(); id[t] = k; }
+  for (int j = 0; j < n; ++j) {
+    const float dx = P[3 * j] - px, dy = P[3 * j + 1] - py, dz = P[3 * j + 2] - pz;
+    float cd = dx * dx + dy * dy + dz * dz;
+    if (j == k || !(cd < d[K - 1])) continue;
+    int cj = j;
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      if (cd < d[t]) {
+        const float td = d[t]; const int tj = id[t];
+        d[t] = cd; id[t] = cj;
+        cd = td; cj = tj;
+      }
+    }
+  }
+  uint16_t* row = nbr + ((int64_t)off[oid] + k) * K;
+#pragma unroll
+  for (int t = 0; t < K; ++t) row[t] = (uint16_t)id[t];
 }
 
 __global__ __launch_bounds__(kThreads) void add_reduce_kernel(
@@ -320,14 +463,33 @@ __global__ __launch_bounds__(kThreads) void add_loss_bwd_kernel(
 
 }  // namespace
 
-extern "C" int pose6d_add_eval(const float* pred_rot, const float* pred_trans, const float* gt_rot,
-                               const float* gt_trans, const int64_t* obj_ids, int64_t B,
-                               const float* points, const int32_t* off, const int32_t* npts,
-                               const uint8_t* sym, const double* diam, int32_t n_slots, int32_t max_npts,
-                               float* min_dist, int32_t* argmin, float* pt_add, double* add, double* adds,
-                               int32_t* valid, int32_t* correct, void* stream) {
+extern "C" int pose6d_add_neighbors(const float* points, const int32_t* off, const int32_t* npts, int32_t n_slots,
+                                    int32_t max_npts, int32_t K, uint16_t* nbr, void* stream) {
+  P6_CHECK_ARG(n_slots >= 0 && max_npts >= 0 && max_npts <= 65536, "pose6d_add_neighbors: bad table sizes");
+  P6_CHECK_ARG(K == 8 || K == 16 || K == 32, "pose6d_add_neighbors: K must be 8, 16 or 32 (got %d)", (int)K);
+  if (n_slots == 0 || max_npts == 0) return POSE6D_OK;
+  P6_CHECK_ARG(points && off && npts && nbr, "pose6d_add_neighbors: null pointer");
+  hipStream_t s = p6::stream_of(stream);
+  const dim3 grid(p6::ceil_div(max_npts, kThreads), (unsigned)n_slots);
+  if (K == 8) add_neighbors_kernel<8><<<grid, kThreads, 0, s>>>(points, off, npts, nbr);
+  else if (K == 16) add_neighbors_kernel<16><<<grid, kThreads, 0, s>>>(points, off, npts, nbr);
+  else add_neighbors_kernel<32><<<grid, kThreads, 0, s>>>(points, off, npts, nbr);
+  P6_LAUNCH_CHECK();
+  return POSE6D_OK;
+}
+
+extern "C" int pose6d_add_eval_nbr(const float* pred_rot, const float* pred_trans, const float* gt_rot,
+                                   const float* gt_trans, const int64_t* obj_ids, int64_t B,
+                                   const float* points, const int32_t* off, const int32_t* npts,
+                                   const uint8_t* sym, const double* diam, int32_t n_slots, int32_t max_npts,
+                                   const uint16_t* nbr, int32_t K, float* min_dist, int32_t* argmin,
+                                   float* pt_add, double* add, double* adds, int32_t* valid, int32_t* correct,
+                                   void* stream) {
   P6_CHECK_ARG(B >= 0 && B <= 65535, "pose6d_add_eval: batch %lld out of range", (long long)B);
   P6_CHECK_ARG(n_slots >= 0 && max_npts >= 0, "pose6d_add_eval: bad table sizes");
+  P6_CHECK_ARG(!nbr || ((K == 8 || K == 16 || K == 32) && max_npts <= 65536 && ((uintptr_t)nbr & 15) == 0),
+               "pose6d_add_eval_nbr: the neighbour table needs K in {8, 16, 32}, <= 65536 points per mesh and "
+               "16-byte alignment");
   if (B == 0) return POSE6D_OK;
   P6_CHECK_ARG(min_dist && pt_add && add && adds && valid && correct, "pose6d_add_eval: null output");
   hipStream_t s = p6::stream_of(stream);
@@ -340,13 +502,24 @@ extern "C" int pose6d_add_eval(const float* pred_rot, const float* pred_trans, c
     dim3 grid(p6::ceil_div(max_npts, kThreads * kPPT), (unsigned)B);
     add_points_kernel<kPPT, 4><<<grid, kThreads, 0, s>>>(pred_rot, pred_trans, gt_rot, gt_trans, obj_ids,
                                                                    points, off, npts, n_slots, max_npts, min_dist,
-                                                                   argmin, pt_add);
+                                                                   argmin, pt_add, nbr, nbr ? K : 0);
     P6_LAUNCH_CHECK();
   }
   add_reduce_kernel<<<(unsigned)B, kThreads, 0, s>>>(obj_ids, npts, sym, diam, n_slots, max_npts, min_dist, pt_add,
                                                       add, adds, valid, correct);
   P6_LAUNCH_CHECK();
   return POSE6D_OK;
+}
+
+extern "C" int pose6d_add_eval(const float* pred_rot, const float* pred_trans, const float* gt_rot,
+                               const float* gt_trans, const int64_t* obj_ids, int64_t B,
+                               const float* points, const int32_t* off, const int32_t* npts,
+                               const uint8_t* sym, const double* diam, int32_t n_slots, int32_t max_npts,
+                               float* min_dist, int32_t* argmin, float* pt_add, double* add, double* adds,
+                               int32_t* valid, int32_t* correct, void* stream) {
+  return pose6d_add_eval_nbr(pred_rot, pred_trans, gt_rot, gt_trans, obj_ids, B, points, off, npts, sym, diam,
+                             n_slots, max_npts, nullptr, 0, min_dist, argmin, pt_add, add, adds, valid, correct,
+                             stream);
 }
 
 extern "C" int pose6d_add_loss_bwd(const float* pred_rot, const float* pred_trans, const float* gt_rot,

@@ -18,6 +18,10 @@ from pose6d._lib import call, require_device, stream
 # LineMOD symmetric objects (eggbox and glue)  -- add_loss.py:10
 SYMMETRIC_OBJECT_IDS = {9, 10}
 
+# neighbours per mesh point in the ADD-S seed table (pose6d_add_neighbors: 8, 16 or 32;
+# 0 = no table).  Only the search's speed depends on it, never its results.
+ADD_SEED_NEIGHBORS = int(os.environ.get("POSE6D_ADD_NEIGHBORS", "16"))
+
 
 class _MeshTable:
     """Packed device copy of ADDLoss.points (+ per-slot diameter / symmetry)."""
@@ -45,6 +49,13 @@ class _MeshTable:
         self.sym = torch.from_numpy(sym).to(device)
         self.diam = torch.from_numpy(diam).to(device)
         self.key = _table_key(points, diameters)
+        # the ADD-S seed table (pose6d_add_eval_nbr), built once per mesh table on the device
+        self.nbr, self.K = None, 0
+        if ADD_SEED_NEIGHBORS and slots and 0 < self.max_npts <= 65536:
+            self.K = ADD_SEED_NEIGHBORS
+            self.nbr = torch.empty(max(cur, 1), self.K, dtype=torch.int16, device=device)
+            call("add_neighbors", self.points, self.off, self.npts, self.n_slots, self.max_npts, self.K, self.nbr,
+                 stream())
 
 
 def _table_key(points, diameters):
@@ -138,8 +149,8 @@ class ADDLoss(nn.Module):
         adds = torch.empty(B, device=dev, dtype=torch.float64)
         valid = torch.empty(B, device=dev, dtype=torch.int32)
         correct = torch.empty(B, device=dev, dtype=torch.int32)
-        call("add_eval", f(pred_r), f(pred_t), f(gt_r), f(gt_t), ids, B, T.points, T.off, T.npts, T.sym, T.diam,
-             T.n_slots, T.max_npts, mind, amin, ptadd, add, adds, valid, correct, stream())
+        call("add_eval_nbr", f(pred_r), f(pred_t), f(gt_r), f(gt_t), ids, B, T.points, T.off, T.npts, T.sym,
+             T.diam, T.n_slots, T.max_npts, T.nbr, T.K, mind, amin, ptadd, add, adds, valid, correct, stream())
         out = {"add": add, "adds": adds, "valid": valid, "correct": correct}
         if want_points:
             out["min"], out["argmin"] = mind, amin

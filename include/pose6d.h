@@ -62,6 +62,27 @@ int pose6d_add_eval(const float *pred_rot, const float *pred_trans, const float 
                     float *min_dist, int32_t *argmin, float *pt_add,
                     double *add, double *adds, int32_t *valid, int32_t *correct, void *stream);
 
+/* pose6d_add_eval with a neighbour table (round 6): nbr [total points][K] uint16
+ * (K = 8, 16 or 32; 16-byte aligned; <= 65536 points per mesh) lists, for every mesh
+ * point, other points of the same mesh near it in model space (pose6d_add_neighbors).
+ * The ADD-S search first visits each point's own ground-truth point and those
+ * neighbours, so the full sweep seldom finds a better candidate; its first-index tie
+ * rule does not depend on the visiting order, so the results are identical (bit for
+ * bit) to pose6d_add_eval whatever the table holds.  nbr == NULL: pose6d_add_eval. */
+int pose6d_add_eval_nbr(const float *pred_rot, const float *pred_trans, const float *gt_rot,
+                        const float *gt_trans, const int64_t *obj_ids, int64_t B,
+                        const float *points, const int32_t *off, const int32_t *npts,
+                        const uint8_t *sym, const double *diam, int32_t n_slots, int32_t max_npts,
+                        const uint16_t *nbr, int32_t K, float *min_dist, int32_t *argmin, float *pt_add,
+                        double *add, double *adds, int32_t *valid, int32_t *correct, void *stream);
+
+/* The neighbour table of a packed mesh table (points / off / npts as pose6d_add_eval):
+ * nbr[off[o] + k][0..K) = the K nearest other points of mesh o to its point k (local
+ * indices; fp32 model-space distances; a mesh of fewer than K + 1 points repeats k).
+ * One launch, a setup step per table (not per evaluation). */
+int pose6d_add_neighbors(const float *points, const int32_t *off, const int32_t *npts, int32_t n_slots,
+                         int32_t max_npts, int32_t K, uint16_t *nbr, void *stream);
+
 /* Backward of ADDLoss.forward (add_loss.py:101-150) w.r.t. the predicted pose:
  * loss = mean over known samples of mean_k ||Q_k - G*_k|| (G* = G_k, or the
  * nearest ground-truth point for SYMMETRIC_OBJECT_IDS, taken from the `argmin`

@@ -195,6 +195,103 @@ __global__ __launch_bounds__(64 * NW) void pipe_kernel(const char* __restrict__ 
   if (v == 12345.f) sink[blockIdx.x * blockDim.x + threadIdx.x] = v;
 }
 
+// register-staged uniform loop (2 LDS slots): stage st+1 sits in VGPRs (global_load_dwordx4,
+// issued D iterations earlier) and is written to the free slot with ds_write_b128 after the
+// fragment reads of stage st are issued; no LDS-DMA at all
+template <int NW, int SLOT, int RPW, int MF, int D>
+__global__ __launch_bounds__(64 * NW) void reg_kernel(const char* __restrict__ buf, size_t mask, int steps, int stride,
+                                                      float* __restrict__ sink) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int PER = SLOT / NW;
+  static_assert(PER * NW == SLOT, "slot must split over the waves");
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const size_t wg_base = (size_t)blockIdx.x * 977 * 1024;
+  const int rowoff = (lane >> 3) * stride + (lane & 7) * 16;
+  auto src_of = [&](int st, int i) {
+    const int piece = i * NW + wave;
+    return reinterpret_cast<const u32x4*>(buf + ((wg_base + (size_t)st * SLOT * 1024 + (size_t)piece * 8 * stride +
+                                                   rowoff) & mask));
+  };
+  auto dst_of = [&](int slot, int i) {
+    return reinterpret_cast<u32x4*>(smem + slot * SLOT * 1024 + (i * NW + wave) * 1024 + lane * 16);
+  };
+  u32x4 regs[D][PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) regs[0][i] = *src_of(0, i);
+#pragma unroll
+  for (int i = 0; i < PER; ++i) *dst_of(0, i) = regs[0][i];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+#pragma unroll
+    for (int i = 0; i < PER; ++i) regs[d][i] = *src_of(1 + d < steps ? 1 + d : steps - 1, i);
+  f32x4 acc[4] = {};
+  for (int st0 = 0; st0 < steps; st0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int st = st0 + d;
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      const char* src = smem + (st & 1) * SLOT * 1024;
+      u32x4 f[RPW];
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) {
+        const int chunk = (wave * RPW + r) * 64 + lane;
+        f[r] = *reinterpret_cast<const u32x4*>(src + (chunk % (SLOT * 64)) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < PER; ++i) *dst_of((st + 1) & 1, i) = regs[d][i];
+      const int nx = st + 1 + D < steps ? st + 1 + D : steps - 1;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) regs[d][i] = *src_of(nx, i);
+      if constexpr (MF >= 0) {
+#pragma unroll
+        for (int m = 0; m < MF; ++m)
+          acc[m & 3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f[m % RPW]),
+                                                               __builtin_bit_cast(bf16x8, f[(m + 1) % RPW]),
+                                                               acc[m & 3], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int m = 0; m < -MF; ++m)
+          acc[m & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(__builtin_bit_cast(f32x4, f[m % RPW])[m & 3],
+                                                            __builtin_bit_cast(f32x4, f[(m + 1) % RPW])[m & 3],
+                                                            acc[m & 3], 0, 0, 0);
+      }
+    }
+  }
+  const float v = acc[0][0] + acc[1][1] + acc[2][2] + acc[3][3];
+  if (v == 12345.f) sink[blockIdx.x * blockDim.x + threadIdx.x] = v;
+}
+
+template <int NW, int SLOT, int RPW, int MF, int D>
+void run_reg(const char* buf, size_t foot, int wpc, float* sink, const char* name) {
+  constexpr int lds = 2 * SLOT * 1024;
+  if (lds * wpc > 160 * 1024 || 64 * NW * wpc > 2048) return;
+  const int grid = 256 * wpc, steps = 60, stride = 2048;
+  auto k = reg_kernel<NW, SLOT, RPW, MF, D>;
+  CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int w = 0; w < 3; ++w) k<<<grid, 64 * NW, lds>>>(buf, foot - 1, steps, stride, sink);
+  CK(hipGetLastError());
+  const int reps = 10;
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) k<<<grid, 64 * NW, lds>>>(buf, foot - 1, steps, stride, sink);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  const double t = ms * 1e-3 / reps;
+  const double per_step_ns = t / steps * 1e9;
+  const double mfma_cyc = (MF >= 0 ? (double)MF * 16 : -(double)MF * 32) * NW * wpc / 4;
+  printf("%-12s NW=%d slot=%2dK D=%d RPW=%2d MF=%2d wpc=%d : %7.2f us  %6.1f ns/stage  %6.1f GB/s/CU  "
+         "MFMA %5.1f%% of the stage (2.4 GHz)\n",
+         name, NW, SLOT, D, RPW, MF, wpc, t * 1e6, per_step_ns / wpc, (double)grid * steps * SLOT * 1024 / t / 256 / 1e9,
+         100.0 * mfma_cyc / (per_step_ns * 2.4));
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+}
+
 template <int NW, int SLOT, int S, int RPW, int MF>
 void run_pipe(const char* buf, size_t foot, int wpc, float* sink, const char* name) {
   constexpr int lds = S * SLOT * 1024;
@@ -256,13 +353,29 @@ void run(const char* buf, size_t foot, int wpc, float* sink, const char* name) {
   CK(hipEventDestroy(e1));
 }
 
-int main() {
+int main(int argc, char** argv) {
   const size_t foot = (size_t)4 << 20;
   char* buf;
   float* sink;
   CK(hipMalloc(&buf, (size_t)64 << 20));
   CK(hipMemset(buf, 0, (size_t)64 << 20));
   CK(hipMalloc(&sink, 1 << 24));
+  if (argc > 1 && argv[1][0] == 'r') {   // register-staged vs LDS-DMA, same tiles
+    for (int wpc = 1; wpc <= 2; ++wpc) {
+      run<0, 4, 16, 3, 8, 8>(buf, foot, wpc, sink, "uni64x64");
+      run_reg<4, 16, 8, 8, 1>(buf, foot, wpc, sink, "reg64x64");
+      run_reg<4, 16, 8, 8, 2>(buf, foot, wpc, sink, "reg64x64");
+      run<0, 8, 32, 3, 12, 16>(buf, foot, wpc, sink, "uni128x128");
+      run_reg<8, 32, 12, 16, 1>(buf, foot, wpc, sink, "reg128x128");
+      run_reg<8, 32, 12, 16, 2>(buf, foot, wpc, sink, "reg128x128");
+      run<0, 4, 16, 3, 8, -32>(buf, foot, wpc, sink, "f32uni64");
+      run_reg<4, 16, 8, -32, 1>(buf, foot, wpc, sink, "f32reg64");
+      run_reg<4, 16, 8, -32, 2>(buf, foot, wpc, sink, "f32reg64");
+    }
+    CK(hipFree(buf));
+    CK(hipFree(sink));
+    return 0;
+  }
   // fp32 64x64 tile (4 waves of 32x32: 32 exact 16x16x4 MFMAs + 8 reads per wave per 16 KiB stage)
   run<0, 4, 16, 3, 8, -32>(buf, foot, 1, sink, "f32uni64");
   run<0, 4, 16, 3, 8, -32>(buf, foot, 2, sink, "f32uni64");
