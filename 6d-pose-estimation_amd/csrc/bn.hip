@@ -19,7 +19,13 @@
 #include "bn_fold.h"
 #include "common.h"
 
+#ifndef POSE6D_FIN_WAVE_ROWS
+#define POSE6D_FIN_WAVE_ROWS 0     // build-time: the training finalize folds <= this many rows per channel on one wave
+                                   // (round 6: 0 -- the whole-workgroup fold is faster at every row count)
+#endif
 namespace {
+
+constexpr int kFinWaveRows = POSE6D_FIN_WAVE_ROWS;
 
 constexpr int kThreads = 256;
 
@@ -599,6 +605,75 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_finalize_kernel(const float* 
   }
 }
 
+// the same finalize with one WORKGROUP per channel (grid.x = C): threads over rows, fp64
+// sums combined by wave_sum and then across the four waves in order by thread 0 -- the
+// one-wave form above is latency-bound on its shuffle / lane-0 tail (the training
+// forward's finalize showed the same: tools/fin_bench.py, profiles/r06_fin_fold.txt)
+__global__ __launch_bounds__(kThreads) void bn_bwd_finalize_wg_kernel(const float* __restrict__ part, int rows, int C,
+                                                                      double count, const float* __restrict__ gamma,
+                                                                      const float* __restrict__ inv,
+                                                                      float* __restrict__ dgamma,
+                                                                      float* __restrict__ dbeta, int accumulate,
+                                                                      float* __restrict__ coef,
+                                                                      BwdFin second_v = BwdFin{}) {
+  __shared__ double red[2][kThreads / 64];
+  if (blockIdx.y == 1) {
+    part = second_v.part; gamma = second_v.gamma; inv = second_v.inv;
+    dgamma = second_v.dgamma; dbeta = second_v.dbeta; coef = second_v.coef;
+  }
+  const int c = blockIdx.x;
+  const int t = threadIdx.x;
+  const float* ps = part + (int64_t)c * rows;
+  const float* pq = part + ((int64_t)C + c) * rows;
+  float g_c = 0.f, i_c = 0.f, db0 = 0.f, dg0 = 0.f;
+  if (t == 0) {
+    g_c = gamma[c];
+    i_c = inv[c];
+    if (accumulate) {
+      if (dbeta) db0 = dbeta[c];
+      if (dgamma) dg0 = dgamma[c];
+    }
+  }
+  double s = 0.0, q = 0.0;
+  int r = t;
+  for (; r + kThreads < rows; r += 2 * kThreads) {
+    const float s0 = ps[r], s1 = ps[r + kThreads], q0 = pq[r], q1 = pq[r + kThreads];
+    s += (double)s0 + (double)s1;
+    q += (double)q0 + (double)q1;
+  }
+  if (r < rows) {
+    s += (double)ps[r];
+    q += (double)pq[r];
+  }
+  s = p6::wave_sum(s);
+  q = p6::wave_sum(q);
+  if ((t & 63) == 0) { red[0][t >> 6] = s; red[1][t >> 6] = q; }
+  __syncthreads();
+  if (t != 0) return;
+  s = 0.0; q = 0.0;
+#pragma unroll
+  for (int w = 0; w < kThreads / 64; ++w) { s += red[0][w]; q += red[1][w]; }
+  if (dbeta) dbeta[c] = db0 + (float)s;
+  if (dgamma) dgamma[c] = dg0 + (float)q;
+  coef[c] = g_c * i_c;
+  coef[C + c] = (float)(s / count);
+  coef[2 * C + c] = (float)(q / count);
+}
+
+#ifndef POSE6D_BWD_FIN_WG
+#define POSE6D_BWD_FIN_WG 1   // build-time: 0 = the one-wave-per-channel backward finalize
+#endif
+void launch_bwd_finalize(const float* part, int rows, int C, int64_t M, const float* gamma, const float* inv,
+                         float* dgamma, float* dbeta, int accumulate, float* coef, const BwdFin& b2, int ny,
+                         hipStream_t s) {
+  if (POSE6D_BWD_FIN_WG)
+    bn_bwd_finalize_wg_kernel<<<dim3(C, ny), kThreads, 0, s>>>(part, rows, C, (double)M, gamma, inv, dgamma, dbeta,
+                                                               accumulate, coef, b2);
+  else
+    bn_bwd_finalize_kernel<<<dim3(p6::ceil_div(C, kThreads / 64), ny), kThreads, 0, s>>>(
+        part, rows, C, (double)M, gamma, inv, dgamma, dbeta, accumulate, coef, b2);
+}
+
 template <typename T, int MK, bool DUAL = false>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const T* __restrict__ dout, const T* __restrict__ out,
                                                                 const float* __restrict__ rs,
@@ -702,7 +777,7 @@ extern "C" int pose6d_bn_finalize(const float* partial, int32_t rows, int32_t C,
   P6_CHECK_ARG(C > 0 && (!training || (rows > 0 && count > 0)), "pose6d_bn_finalize: bad sizes");
   hipStream_t s = p6::stream_of(stream);
   if (training) {
-    if (rows > 512)
+    if (rows > kFinWaveRows)
       bn_stats_finalize_kernel<256><<<C, kThreads, 0, s>>>(partial, rows, C, count, gamma, beta, running_mean,
                                                             running_var, num_batches, momentum, eps, scale, shift,
                                                             save_mean, save_invstd);
@@ -725,7 +800,7 @@ extern "C" int pose6d_bn_finalize_dual(const pose6d_bn_stats_t* a, const pose6d_
                "pose6d_bn_finalize_dual: bad sizes");
   hipStream_t s = p6::stream_of(stream);
   const int cmax = a->C > b->C ? a->C : b->C;
-  if (rows > 512)
+  if (rows > kFinWaveRows)
     bn_stats_finalize2_kernel<256><<<dim3(cmax, 2), kThreads, 0, s>>>(*a, *b, rows, count);
   else
     bn_stats_finalize2_kernel<64><<<dim3(p6::ceil_div(cmax, 4), 2), kThreads, 0, s>>>(*a, *b, rows, count);
@@ -752,7 +827,7 @@ extern "C" int pose6d_bn_act_fwd_mask(int32_t dtype, const void* y, const float*
 
 // ready flags one pose6d_bn_finalize_act launch needs (int32, zeroed once by the caller)
 extern "C" int32_t pose6d_bn_finalize_act_flags(int32_t rows, int32_t C) {
-  return rows > 512 ? C : (C + 3) / 4;
+  return rows > kFinWaveRows ? C : (C + 3) / 4;
 }
 
 extern "C" int pose6d_bn_finalize_act(int32_t dtype, const pose6d_bn_stats_t* bn, int32_t rows, int64_t count,
@@ -772,7 +847,7 @@ extern "C" int pose6d_bn_finalize_act(int32_t dtype, const pose6d_bn_stats_t* bn
     constexpr int RPB = kThreads / (kFinGroup / V<TT>::E);
     const int64_t napp = (int64_t)(C / kFinGroup) * p6::ceil_div(count, RPB);
     const unsigned grid = (unsigned)(nfin + napp);
-    if (rows > 512)
+    if (rows > kFinWaveRows)
       bn_fin_act_kernel<TT, 256><<<grid, kThreads, 0, s>>>(*bn, rows, count, nfin, (const TT*)y, (const TT*)res, relu,
                                                            (TT*)out, relu_mask, flags, epoch);
     else
@@ -844,8 +919,7 @@ int bn_bwd_impl(int mk, int32_t dtype, const void* dout, const void* out, const 
   if (dtype == POSE6D_DT_BF16) reduce((bf16*)nullptr);
   else reduce((float*)nullptr);
   P6_LAUNCH_CHECK();
-  bn_bwd_finalize_kernel<<<p6::ceil_div(C, kThreads / 64), kThreads, 0, s>>>(part, nb, C, (double)M, gamma, invstd, dgamma, dbeta,
-                                                                  accumulate, coef);
+  launch_bwd_finalize(part, nb, C, M, gamma, invstd, dgamma, dbeta, accumulate, coef, BwdFin{}, 1, s);
   P6_LAUNCH_CHECK();
   auto apply = [&](auto* typed) {
     using TT = std::remove_pointer_t<decltype(typed)>;
@@ -883,8 +957,7 @@ extern "C" int pose6d_bn_bwd_partials(int32_t dtype, const float* partial, int32
   hipStream_t s = p6::stream_of(stream);
   float* coef2 = coef + 3 * (int64_t)C;
   const BwdFin b2{partial2, gamma2, invstd2, dgamma2, dbeta2, coef2};
-  bn_bwd_finalize_kernel<<<dim3(p6::ceil_div(C, kThreads / 64), dual ? 2 : 1), kThreads, 0, s>>>(
-      partial, rows, C, (double)M, gamma, invstd, dgamma, dbeta, accumulate, coef, b2);
+  launch_bwd_finalize(partial, rows, C, M, gamma, invstd, dgamma, dbeta, accumulate, coef, b2, dual ? 2 : 1, s);
   P6_LAUNCH_CHECK();
   auto apply = [&](auto* typed) {
     using TT = std::remove_pointer_t<decltype(typed)>;
@@ -940,8 +1013,7 @@ extern "C" int pose6d_bn_bwd_mask_dual(int32_t dtype, const void* dout, const ui
   else run((float*)nullptr);
   P6_LAUNCH_CHECK();
   const BwdFin b2{part2, gamma2, invstd2, dgamma2, dbeta2, coef2};
-  bn_bwd_finalize_kernel<<<dim3(p6::ceil_div(C, kThreads / 64), 2), kThreads, 0, s>>>(
-      part, nb, C, (double)M, gamma, invstd, dgamma, dbeta, accumulate, coef, b2);
+  launch_bwd_finalize(part, nb, C, M, gamma, invstd, dgamma, dbeta, accumulate, coef, b2, 2, s);
   P6_LAUNCH_CHECK();
   auto apply = [&](auto* typed) {
     using TT = std::remove_pointer_t<decltype(typed)>;
