@@ -29,7 +29,7 @@
 #define POSE6D_ADD_HIT 1   // build-time: 0 = timing-only build, the minimum updates skipped (wrong results)
 #endif
 #ifndef POSE6D_ADD_SEED
-#define POSE6D_ADD_SEED 1  // build-time: 1 = every point's minimum starts at its own ground-truth point
+#define POSE6D_ADD_SEED 1  // build-time: 0 = never seed (the neighbour table is ignored)
 #endif
 #ifndef POSE6D_ADD_HOPS
 #define POSE6D_ADD_HOPS 2  // build-time: neighbour-table hops of the seed walk (1 = the point's own row only)
@@ -90,10 +90,13 @@ __device__ __forceinline__ float sqdist(float ax, float ay, float az, float4 g) 
 // squared distances of a trip are independent chains (3 sub, mul, 2 fma each), and
 // ONE compare-and-branch per trip asks whether any of them beat its running minimum
 // -- after the first few hundred ground-truth points almost never -- instead of a
-// branch per (point, gt point).  The rare update replays the trip's candidates
-// through `update`, whose first-index tie rule does not depend on the visiting order
-// (the sweep starts from the point's own ground-truth point, POSE6D_ADD_SEED).
-template <int PPT, int U>
+// branch per (point, gt point).  The rare update replays the trip's candidates.
+//   SEED = false: the plain in-order sweep (pose6d_add_eval without a neighbour table);
+//          a new squared minimum keeps the old, earlier index iff the roots are equal.
+//   SEED = true: the minimum starts from the point's own ground-truth point and a walk
+//          on the mesh's neighbour table, so the sweep seldom finds a better candidate;
+//          the tie rule is then order-free (below), so the bits are the same.
+template <int PPT, int U, bool SEED>
 __global__ __launch_bounds__(kThreads) void add_points_kernel(
     const float* __restrict__ pred_rot, const float* __restrict__ pred_trans,
     const float* __restrict__ gt_rot, const float* __restrict__ gt_trans,
@@ -118,9 +121,9 @@ __global__ __launch_bounds__(kThreads) void add_points_kernel(
 
   // best = smallest squared distance seen, bi = the SMALLEST index among the seen
   // candidates whose sqrtf equals sqrtf(best) (the reference's first-index argmin over
-  // the roots), thr = the largest squared distance that can still matter: a root equal
-  // to sqrtf(best) needs the two within 2^-20 relative (a correctly rounded sqrt of
-  // values farther apart differs by >= 8 ulps of the root), so thr = best (1 + 2^-19).
+  // the roots); SEED: thr = the largest squared distance that can still matter -- a root
+  // equal to sqrtf(best) needs the two within 2^-20 relative (a correctly rounded sqrt
+  // of values farther apart differs by >= 8 ulps of the root), so thr = best (1 + 2^-19).
   float qx[PPT], qy[PPT], qz[PPT], best[PPT], thr[PPT];
   int bi[PPT];
 #pragma unroll
@@ -135,95 +138,73 @@ __global__ __launch_bounds__(kThreads) void add_points_kernel(
       const float4 g = xform(P + 3 * k, Rg, tg, n);
       const float skk = sqdist(q.x, q.y, q.z, g);
       pt_add[(int64_t)b * max_npts + k] = sqrtf(skk);  // add_loss.py:182
-#if POSE6D_ADD_SEED
-      // seed: the point's own ground-truth point (the ADD pair, already at hand) -- for
-      // a pose near the truth it is near the nearest one, so the sweep below seldom
-      // finds a better candidate and its per-trip test almost never branches.  The
-      // sweep then sees j < k after k, which the order-free rule of `update` handles.
-      // (NaN distances never become a minimum, as in the sweep: `s < best` is false.)
-      if (skk == skk) { best[i] = skk; bi[i] = k; }
-#endif
+      // SEED: the point's own ground-truth point (the ADD pair, already at hand) is the
+      // first candidate (NaN never becomes a minimum, as in the sweep)
+      if (SEED && skk == skk) { best[i] = skk; bi[i] = k; }
     } else {
       best[i] = -__builtin_inff();   // idle lane: nothing beats it (its result is never stored)
     }
     thr[i] = best[i] + best[i] * 0x1p-19f;
   }
 
-  // order-free: the result is the same for any visiting order of the j's.  A new
-  // squared minimum keeps the old index (or takes j if smaller) iff sqrtf maps both to
-  // the same value, which needs them within 2^-20 relative, so the two square roots are
-  // taken only then -- the common update is a subtract, a multiply and a compare; a
-  // candidate in [best, thr] is a possible root tie and wins only with a smaller index
+  // in order (SEED = false): the common update is a subtract, a multiply and a compare;
+  // the two square roots are taken only when the minima are within 2^-20 relative.
+  // order-free (SEED): a new squared minimum keeps the old index, or takes j if smaller,
+  // iff the roots are equal; a candidate in [best, thr] is a possible root tie and wins
+  // only with a smaller index.
   auto update = [&](int i, float s, int j) {
     if (s < best[i]) {
       const float gap = best[i] - s;   // exact when the two are close (Sterbenz)
       if (!(gap <= best[i] * 0x1p-20f) || sqrtf(s) != sqrtf(best[i])) bi[i] = j;
-      else bi[i] = min(bi[i], j);
+      else if (SEED) bi[i] = min(bi[i], j);
       best[i] = s;
-      thr[i] = s + s * 0x1p-19f;
-    } else if (j < bi[i] && s <= thr[i] && sqrtf(s) == sqrtf(best[i])) {
+      if (SEED) thr[i] = s + s * 0x1p-19f;
+    } else if (SEED && j < bi[i] && s <= thr[i] && sqrtf(s) == sqrtf(best[i])) {
       bi[i] = j;
     }
   };
-  bool tile_ready = false;   // the mesh's only tile already in LDS (seeded from it)
-#if POSE6D_ADD_SEED
-  // seeds, part 2: the point's K nearest mesh neighbours in model space
-  // (pose6d_add_neighbors, [point][K] local indices) -- the nearest transformed ground-
-  // truth point of a near-truth pose is almost always among them, so after these the
-  // sweep's per-trip test seldom fires.  Each seed is a genuine candidate (index
-  // clamped into the mesh, distance computed as the sweep computes it), so a poor or
-  // even wrong table costs time, never bits.
-  if (nbr != nullptr) {
-    if (n <= kTile) {
-      for (int jj = tid; jj < n; jj += kThreads) gs[jj] = xform(P + 3 * jj, Rg, tg, n);
-      __syncthreads();
-      tile_ready = true;
-    }
+  // the first tile goes to LDS before the seeds (they read it when the mesh fits one tile)
+  for (int jj = tid; jj < min(kTile, n); jj += kThreads) gs[jj] = xform(P + 3 * jj, Rg, tg, n);
+  __syncthreads();
+  if constexpr (SEED) {
+    // the point's neighbours in model space (pose6d_add_neighbors, [point][K] local
+    // indices) in a greedy walk: the row of the point's own index, then the row of the
+    // best candidate found so far while that keeps moving (the nearest transformed point
+    // sits near x = Rg^T (q - tg) in model space, a short walk from k).  Every seed is a
+    // genuine candidate (index clamped into the mesh, distance computed as the sweep
+    // computes it), so a poor or even wrong table costs time, never bits.
     const uint16_t* nb = nbr + (int64_t)off[oid] * K;
+    const bool in_lds = n <= kTile;
+    auto cand = [&](int j) { return in_lds ? gs[j] : xform(P + 3 * j, Rg, tg, n); };
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
       const int k = base + tid + kThreads * i;
       if (k >= n) continue;
-      // a greedy walk on the neighbour graph: the row of the point's own index, then the
-      // row of the best candidate found so far while that keeps moving (the nearest
-      // transformed point sits near x = Rg^T (q - tg) in model space, a short walk from k)
       int cur = k;
       for (int h = 0; h < POSE6D_ADD_HOPS; ++h) {
         const uint16_t* row = nb + (int64_t)cur * K;
         for (int t = 0; t < K; t += 8) {
           const uint4 w = *reinterpret_cast<const uint4*>(row + t);   // 8 indices (K % 8 == 0, 16-B rows)
           const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-          float sv[8];
-          int jv[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int j = min((int)((ww[e >> 1] >> (16 * (e & 1))) & 0xffffu), n - 1);
-            const float4 g = tile_ready ? gs[j] : xform(P + 3 * j, Rg, tg, n);
-            sv[e] = sqdist(qx[i], qy[i], qz[i], g);
-            jv[e] = j;
+          for (int e2 = 0; e2 < 4; ++e2) {   // two candidates at a time (register footprint)
+            const int ja = min((int)(ww[e2] & 0xffffu), n - 1), jb = min((int)(ww[e2] >> 16), n - 1);
+            const float sa = sqdist(qx[i], qy[i], qz[i], cand(ja)), sb = sqdist(qx[i], qy[i], qz[i], cand(jb));
+            update(i, sa, ja);
+            update(i, sb, jb);
           }
-#pragma unroll
-          for (int e = 0; e < 8; ++e) update(i, sv[e], jv[e]);
         }
         if (bi[i] == cur) break;   // nothing nearer around cur
         cur = bi[i];
       }
+      // the candidates of the best's own trip that precede it (<= U - 1 of them): the
+      // sweep's trip test only asks for strict improvements there (see below)
+      for (int j = bi[i] & ~(U - 1); j < bi[i]; ++j) update(i, sqdist(qx[i], qy[i], qz[i], cand(j)), j);
     }
   }
-  // the candidates of the best's own trip that precede it (<= U - 1 of them): the
-  // sweep's trip test only asks for strict improvements there (see below)
-#pragma unroll
-  for (int i = 0; i < PPT; ++i) {
-    if (base + tid + kThreads * i >= n) continue;
-    for (int j = bi[i] & ~(U - 1); j < bi[i]; ++j) {
-      const float4 g = tile_ready ? gs[j] : xform(P + 3 * j, Rg, tg, n);
-      update(i, sqdist(qx[i], qy[i], qz[i], g), j);
-    }
-  }
-#endif
   for (int j0 = 0; j0 < n; j0 += kTile) {
     const int jn = min(kTile, n - j0);
-    if (!tile_ready) {
+    if (j0 > 0) {
       __syncthreads();
       for (int jj = tid; jj < jn; jj += kThreads) gs[jj] = xform(P + 3 * (j0 + jj), Rg, tg, n);
       __syncthreads();
@@ -242,21 +223,21 @@ __global__ __launch_bounds__(kThreads) void add_points_kernel(
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int i = 0; i < PPT; ++i) s[u][i] = sqdist(qx[i], qy[i], qz[i], g[u]);
-      // min over the trip first (v_min3), one compare per point: any s <= thr <=> min(s) <= thr
+      // min over the trip first (v_min3), one compare per point: any s < best <=> min(s) < best
+      // (SEED: any s <= thr <=> min(s) <= thr)
       float m[PPT];
 #pragma unroll
       for (int i = 0; i < PPT; ++i) {
         m[i] = s[0][i];
 #pragma unroll
         for (int u = 1; u < U; ++u) m[i] = __builtin_fminf(m[i], s[u][i]);
-        hit |= __ballot(m[i] <= thr[i]);
+        hit |= __ballot(SEED ? m[i] <= thr[i] : m[i] < best[i]);
       }
 #if POSE6D_ADD_HIT == 0
       (void)m;   // timing-only build: the updates skipped (wrong results)
       if (hit == 0x1234567ull) best[0] = 0.f;
 #else
-      if (__builtin_expect(hit != 0, 0)) {
-#if POSE6D_ADD_SEED
+      if (SEED && __builtin_expect(hit != 0, 0)) {
         // most of these are a point meeting its own current best (m == best <= thr):
         // only a trip wholly before the best's trip can hold a root tie that wins (a
         // smaller index), so elsewhere only a strict improvement counts.  (The best's
@@ -269,8 +250,7 @@ __global__ __launch_bounds__(kThreads) void add_points_kernel(
           real |= __ballot(m[i] < best[i] || (jb < (bi[i] & ~(U - 1)) && m[i] <= thr[i]));
         hit = real;
       }
-      if (hit != 0) {
-#endif
+      if (__builtin_expect(hit != 0, 0)) {
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -500,9 +480,14 @@ extern "C" int pose6d_add_eval_nbr(const float* pred_rot, const float* pred_tran
     // the waves per SIMD) were all slower
     constexpr int kPPT = 2;
     dim3 grid(p6::ceil_div(max_npts, kThreads * kPPT), (unsigned)B);
-    add_points_kernel<kPPT, 4><<<grid, kThreads, 0, s>>>(pred_rot, pred_trans, gt_rot, gt_trans, obj_ids,
-                                                                   points, off, npts, n_slots, max_npts, min_dist,
-                                                                   argmin, pt_add, nbr, nbr ? K : 0);
+    if (nbr && POSE6D_ADD_SEED)
+      add_points_kernel<kPPT, 4, true><<<grid, kThreads, 0, s>>>(pred_rot, pred_trans, gt_rot, gt_trans, obj_ids,
+                                                                 points, off, npts, n_slots, max_npts, min_dist,
+                                                                 argmin, pt_add, nbr, K);
+    else
+      add_points_kernel<kPPT, 4, false><<<grid, kThreads, 0, s>>>(pred_rot, pred_trans, gt_rot, gt_trans, obj_ids,
+                                                                  points, off, npts, n_slots, max_npts, min_dist,
+                                                                  argmin, pt_add, nullptr, 0);
     P6_LAUNCH_CHECK();
   }
   add_reduce_kernel<<<(unsigned)B, kThreads, 0, s>>>(obj_ids, npts, sym, diam, n_slots, max_npts, min_dist, pt_add,

@@ -149,8 +149,12 @@ class ADDLoss(nn.Module):
         adds = torch.empty(B, device=dev, dtype=torch.float64)
         valid = torch.empty(B, device=dev, dtype=torch.int32)
         correct = torch.empty(B, device=dev, dtype=torch.int32)
-        call("add_eval_nbr", f(pred_r), f(pred_t), f(gt_r), f(gt_t), ids, B, T.points, T.off, T.npts, T.sym,
-             T.diam, T.n_slots, T.max_npts, T.nbr, T.K, mind, amin, ptadd, add, adds, valid, correct, stream())
+        if T.nbr is None:
+            call("add_eval", f(pred_r), f(pred_t), f(gt_r), f(gt_t), ids, B, T.points, T.off, T.npts, T.sym,
+                 T.diam, T.n_slots, T.max_npts, mind, amin, ptadd, add, adds, valid, correct, stream())
+        else:
+            call("add_eval_nbr", f(pred_r), f(pred_t), f(gt_r), f(gt_t), ids, B, T.points, T.off, T.npts, T.sym,
+                 T.diam, T.n_slots, T.max_npts, T.nbr, T.K, mind, amin, ptadd, add, adds, valid, correct, stream())
         out = {"add": add, "adds": adds, "valid": valid, "correct": correct}
         if want_points:
             out["min"], out["argmin"] = mind, amin
