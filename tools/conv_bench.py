@@ -110,6 +110,10 @@ def main():
         flops = 2.0 * B * Ho * Wo * Cout * Cin * k * k
         sc, sh = torch.rand(Cout, device=dev) + 0.5, torch.randn(Cout, device=dev) * 0.1
         res = torch.randn(B, Ho, Wo, Cout, device=dev).to(dtype) if "fwdactres" in a.passes else None
+        # the residual junction's gradient added in the data-gradient epilogue (bwdres*)
+        dres = torch.randn(B, H, W, Cin, device=dev).to(dtype) if "bwdres" in a.passes else None
+        if "bwdrescold" in a.passes and flush is None:
+            flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
         fns = {
             "fwd": lambda: call("conv2d_fwd_tuned", dt, x, wp, None, y, stats, B, H, W, Cin, Cout, k, k, s, p, Ho,
                                 Wo, TUNE.ref, skw, skw.numel(), stream()),
@@ -135,14 +139,20 @@ def main():
                                   Cin, Cout, k, k, s, p, Ho, Wo, stream()),
             "bwd": lambda: call("conv2d_backward_tuned", dt, x, dy, wt, None, dx, dw, 0, ws, ws.numel() * 4, B, H, W,
                                 Cin, Cin, Cout, k, k, s, p, Ho, Wo, TUNE.ref, stream()),
+            "bwdres": lambda: call("conv2d_backward_tuned", dt, x, dy, wt, dres, dx, dw, 0, ws, ws.numel() * 4, B, H,
+                                   W, Cin, Cin, Cout, k, k, s, p, Ho, Wo, TUNE.ref, stream()),
+            # behind a 512 MB write (operands from HBM, as in the step), minus that write's time (--passes flush)
+            "bwdrescold": lambda: (flush.zero_(), call("conv2d_backward_tuned", dt, x, dy, wt, dres, dx, dw, 0, ws,
+                                                       ws.numel() * 4, B, H, W, Cin, Cin, Cout, k, k, s, p, Ho, Wo,
+                                                       TUNE.ref, stream())),
             "wgrad": lambda: call("conv2d_wgrad_tuned", dt, x, dy, dw, 0, ws, ws.numel() * 4, B, H, W, Cin, Cin, Cout,
                                   k, k, s, p, Ho, Wo, TUNE.ref, stream()),
         }
         line = f"{H:3d}x{W:<3d} {Cin:4d}->{Cout:<4d} k{k}s{s} |"
-        if "fwdcold" in a.passes.split(","):
+        if "fwdcold" in a.passes.split(",") or "bwdrescold" in a.passes.split(","):
             line += f" flush:{timeit(fns['flush']) * 1e6:6.1f}us"
         for ps in a.passes.split(","):
-            if ps in ("dgrad", "bwd", "dgradip", "bwdip") and Cin % 8:
+            if ps in ("dgrad", "bwd", "dgradip", "bwdip", "bwdres", "bwdrescold") and Cin % 8:
                 continue   # the stem has no data gradient
             sweep = a.wgrad_env if ps == "wgrad" else a.env
             if sweep:
@@ -153,8 +163,9 @@ def main():
                     _set_tune()
                     line += f" {ps[0]}[{spec}]:{sec * 1e6:6.1f}us/{flops / sec / 1e12:5.0f}T"
                 continue
-            impls = {"wgrad": ["base"], "bwd": ["fast"], "bwdip": ["fast"]}.get(ps, a.impls.split(","))
-            tiles = a.tiles.split(",") if ps not in ("wgrad", "bwd", "bwdip") else ["auto"]
+            impls = {"wgrad": ["base"], "bwd": ["fast"], "bwdip": ["fast"], "bwdres": ["fast"],
+                     "bwdrescold": ["fast"]}.get(ps, a.impls.split(","))
+            tiles = a.tiles.split(",") if ps not in ("wgrad", "bwd", "bwdip", "bwdres", "bwdrescold") else ["auto"]
             for impl in impls:
                 stages = a.stages.split(",") if impl == "fast" else ["auto"]
                 for t in tiles:
