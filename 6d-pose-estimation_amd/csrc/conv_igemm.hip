@@ -1582,12 +1582,19 @@ bool s2_ok(const Geom& g) {
 // and 95.2 -> 83.7 us (profiles/r04_f32_conv_sweep.txt).  Everywhere else the merge (write-through partial stores, the
 // arrival atomic, the partial reads: ~3-5 us on the last arriver's critical path)
 // costs more than the shorter K loop saves (profiles/r04_splitk_sweep.txt).
+#ifndef POSE6D_SPLITK_SMALL_TILES
+#define POSE6D_SPLITK_SMALL_TILES 64   // build-time (A/B): 0 = the batch-32 rule only
+#endif
 int default_splits(int dtype, int mode, const Geom& g, bool fused) {
   if (fused || !(mode == kGemm || mode == kFwd || mode == kDgrad)) return 1;
   (void)dtype;
   const int ks = dtype == POSE6D_DT_BF16 ? 64 : 32;
   const int nk = fast_nk(mode, g, ks);
   const int64_t tiles64 = (int64_t)p6::ceil_div(g.M, 64) * p6::ceil_div(g.Ncols, 64);
+  // small grids (batch 1-2: at most a quarter of the CUs busy) with >= 16 K-steps: four
+  // shorter K walks per tile (B = 1 eval forwards 7.7 -> 7.1 us on 14x14 1024->256, 14.4 ->
+  // 10.6 us on layer4's 3x3; profiles/r06_b1_splitk.txt); no batch-32 conv has <= 64 tiles
+  if (nk >= 16 && tiles64 <= POSE6D_SPLITK_SMALL_TILES) return 4;
   if (nk >= 32 && tiles64 <= 256) return 2;
   return 1;
 }
