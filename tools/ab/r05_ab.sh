@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU suite (patch tests first), eval per-layer times (new vs ab/libpose6d_old.so), A/B of
-# the bf16 training step and of the eval forward.  usage: bash tools/r05_ab.sh TAG [rounds]
+# the bf16 training step and of the eval forward.  usage: bash tools/ab/r05_ab.sh TAG [rounds]
 TAG=${1:-r05c}; R=${2:-3}
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Conv-level diagnostics of the 3x3 forwards: graph-timed ring-depth sweep of the patch
 # kernel against the implicit GEMM, then PMC passes (one counter group per run) on the
-# layer3 and layer4 3x3 shapes.  usage: bash tools/r05_convdiag.sh TAG
+# layer3 and layer4 3x3 shapes.  usage: bash tools/ab/r05_convdiag.sh TAG
 TAG=${1:-r05d}
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp

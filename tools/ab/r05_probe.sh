@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-5 probe: GPU suite, eval-forward per-layer times for each ab/ variant library,
-# PMC passes over the eager eval forward.  usage: bash tools/r05_probe.sh TAG [variants...]
+# PMC passes over the eager eval forward.  usage: bash tools/ab/r05_probe.sh TAG [variants...]
 TAG=${1:-r05b}; shift
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp

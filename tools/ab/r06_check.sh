@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-6 GPU check: the tests this round touched first (verbose), then the whole GPU
-# suite, then the default bench line.  usage: bash tools/r06_check.sh TAG [--no-bench]
+# suite, then the default bench line.  usage: bash tools/ab/r06_check.sh TAG [--no-bench]
 set -o pipefail
 TAG=${1:-r06a}
 cd "$GRAFT_REPO_ROOT" || exit 1

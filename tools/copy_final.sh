@@ -1,5 +1,5 @@
 #!/bin/bash
-# copy a tools/r06_final.sh run's outputs from gpurun_out/ into profiles/ (TAG_*)
+# copy a tools/ab/r06_final.sh run's outputs from gpurun_out/ into profiles/ (TAG_*)
 T=${1:?tag}
 set -e
 cp gpurun_out/$T/bench.json profiles/${T}_bench.json
