@@ -433,6 +433,18 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
 #define POSE6D_WGRAD_F32_ONE_SPLIT_TILES 256   // build-time (A/B)
 #endif
   if (p.fast && dtype == POSE6D_DT_F32 && p.bm == 64 && tiles >= POSE6D_WGRAD_F32_ONE_SPLIT_TILES) target = tiles;
+#ifndef POSE6D_WGRAD_BF128_ONE_SPLIT_TILES
+#define POSE6D_WGRAD_BF128_ONE_SPLIT_TILES 128   // bf16 128x128 plans with >= this many tiles (layer4 3x3): one split
+                                                 // (no slab round trip in the next launch: 4.532 -> 4.515 ms, profiles/r06_l4_onesplit.txt)
+#endif
+#ifndef POSE6D_WGRAD_BF128_TARGET
+#define POSE6D_WGRAD_BF128_TARGET 0   // build-time (A/B): workgroup target of the bf16 128x128 plans (0 = the KxK target)
+#endif
+  if (POSE6D_WGRAD_BF128_TARGET > 0 && p.fast && dtype == POSE6D_DT_BF16 && p.bm == 128)
+    target = POSE6D_WGRAD_BF128_TARGET;
+  if (POSE6D_WGRAD_BF128_ONE_SPLIT_TILES > 0 && p.fast && dtype == POSE6D_DT_BF16 && p.bm == 128 &&
+      tiles >= POSE6D_WGRAD_BF128_ONE_SPLIT_TILES)
+    target = tiles;
   // aim for ~`target` workgroups, each reducing >= min_rows pixels, slabs capped in bytes
   int splits = p6::ceil_div(target, tiles);
   const int max_splits = p6::ceil_div(M, min_rows);
