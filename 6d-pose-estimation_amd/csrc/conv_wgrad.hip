@@ -423,7 +423,8 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
   // take twice the workgroups: 8 splits of 196 pixels, 207 -> 184 us on 7x7 512->512;
   // the few-tile KxK shapes keep the default target (profiles/r04_fp32_kxk_splits.txt)
 #ifndef POSE6D_WGRAD_F32_MANY_TILES
-#define POSE6D_WGRAD_F32_MANY_TILES 128   // build-time (A/B): tiles from which the target doubles
+#define POSE6D_WGRAD_F32_MANY_TILES 100000   // build-time (A/B): tiles from which the target doubles (round 6: off -- neutral to -0.2 %
+                                           // the doubled slabs are read back by the next launch; profiles/r06_f32_split.txt)
 #endif
   if (p.fast && dtype == POSE6D_DT_F32 && p.bm == 128 && tiles >= POSE6D_WGRAD_F32_MANY_TILES) target *= 2;
   // fp32 64x64 plans with >= 256 tiles (layer4's 512 -> 2048 / 2048 -> 512 1x1 convs): one
@@ -437,6 +438,12 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
 #define POSE6D_WGRAD_BF128_ONE_SPLIT_TILES 128   // bf16 128x128 plans with >= this many tiles (layer4 3x3): one split
                                                  // (no slab round trip in the next launch: 4.532 -> 4.515 ms, profiles/r06_l4_onesplit.txt)
 #endif
+#ifndef POSE6D_WGRAD_F32_128_ONE_SPLIT_TILES
+#define POSE6D_WGRAD_F32_128_ONE_SPLIT_TILES 0   // build-time (A/B): fp32 128x128 plans with >= this many tiles: one split
+#endif
+  if (POSE6D_WGRAD_F32_128_ONE_SPLIT_TILES > 0 && p.fast && dtype == POSE6D_DT_F32 && p.bm == 128 &&
+      tiles >= POSE6D_WGRAD_F32_128_ONE_SPLIT_TILES)
+    target = tiles;
 #ifndef POSE6D_WGRAD_BF128_TARGET
 #define POSE6D_WGRAD_BF128_TARGET 0   // build-time (A/B): workgroup target of the bf16 128x128 plans (0 = the KxK target)
 #endif
