@@ -444,6 +444,11 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
   if (POSE6D_WGRAD_F32_128_ONE_SPLIT_TILES > 0 && p.fast && dtype == POSE6D_DT_F32 && p.bm == 128 &&
       tiles >= POSE6D_WGRAD_F32_128_ONE_SPLIT_TILES)
     target = tiles;
+#ifndef POSE6D_WGRAD_F32_128_TARGET
+#define POSE6D_WGRAD_F32_128_TARGET 0   // build-time (A/B): workgroup target of the fp32 128x128 plans (0 = default)
+#endif
+  if (POSE6D_WGRAD_F32_128_TARGET > 0 && p.fast && dtype == POSE6D_DT_F32 && p.bm == 128)
+    target = POSE6D_WGRAD_F32_128_TARGET;
 #ifndef POSE6D_WGRAD_BF128_TARGET
 #define POSE6D_WGRAD_BF128_TARGET 192   // workgroup target of the bf16 128x128 plans (0 = the KxK target, 256): fewer
                                         // slabs for the next launch to read back (profiles/r06_bf128_target.txt)
