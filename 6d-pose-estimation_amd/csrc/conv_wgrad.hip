@@ -388,7 +388,10 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
   } else if (p.fast) {
     p.bm = bf128 ? 128 : 64;
     p.bn = bf128 ? 128 : 64;
-    p.stages = tuned(tn, &pose6d_tuning_t::wgrad_stages, bf128 ? 2 : POSE6D_WGRAD_STAGES);
+#ifndef POSE6D_WGRAD_STAGES_BF128
+#define POSE6D_WGRAD_STAGES_BF128 2   // build-time (A/B): ring slots of the bf16 128x128 weight gradient
+#endif
+    p.stages = tuned(tn, &pose6d_tuning_t::wgrad_stages, bf128 ? POSE6D_WGRAD_STAGES_BF128 : POSE6D_WGRAD_STAGES);
     if (p.stages < 2) p.stages = 2;
     if (p.stages > (bf128 ? 3 : 4)) p.stages = bf128 ? 3 : 4;
     // ~256 workgroups (one per CU): with the fused launch dispatching its longest
