@@ -2068,6 +2068,9 @@ template <int DMODE>
 int launch_bwd8_mode(int ds, int ws_stages, const Geom& gd, const p6::WGeom& gw, const void* dy, const void* wt,
                      const void* dres, void* dx, const void* x, float* ws, const ReduceJob& rj, hipStream_t s,
                      int order) {
+#ifdef POSE6D_BWD8_DS   // build-time (A/B): force the 8-wave fused launch's data-gradient ring depth
+  ds = POSE6D_BWD8_DS;
+#endif
   if (ws_stages >= 3)
     return ds == 2 ? launch_bwd8<DMODE, 2, 3>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order)
                    : launch_bwd8<DMODE, 4, 3>(gd, gw, dy, wt, dres, dx, x, ws, rj, s, order);
