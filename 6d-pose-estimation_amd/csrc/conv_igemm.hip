@@ -2055,7 +2055,10 @@ int launch_bwd8(const Geom& gd0, const p6::WGeom& gw, const void* dy, const void
   int lds = ring_d > epi ? ring_d : epi;
   lds = lds > ring_w ? lds : ring_w;
   lds = lds > acc_stage_bytes<128, 128>() ? lds : acc_stage_bytes<128, 128>();
-  const int wfirst = order >= 0 ? order : (POSE6D_BWD_ORDER == 2 || (POSE6D_BWD_ORDER && p6::ceil_div(gw.mps, 64) >= nk));
+#ifndef POSE6D_BWD8_ORDER
+#define POSE6D_BWD8_ORDER POSE6D_BWD_ORDER   // build-time (A/B): the 8-wave launch's order rule (as POSE6D_BWD_ORDER)
+#endif
+  const int wfirst = order >= 0 ? order : (POSE6D_BWD8_ORDER == 2 || (POSE6D_BWD8_ORDER && p6::ceil_div(gw.mps, 64) >= nk));
   const int grid = wfirst ? ((nw + 7) & ~7) + nd + rj.nblk : nd_pad + nw + rj.nblk;
   conv_bwd8_kernel<DMODE, DS, WS><<<grid, 2 * kThreads, lds, s>>>(
       (const bf16*)dy, (const bf16*)wt, (const bf16*)dres, (bf16*)dx, gd, nd, nd_pad, wfirst, (const bf16*)x, ws, gw,
