@@ -59,6 +59,13 @@ def test_conv_plan_query_reports_split_k():
         assert splits(dt, 0, 32, 14, 256, 1024, 1, 1) == 1    # short K
     for dt in (DT_BF16, DT_F32):                             # data gradients: split only when tuned
         assert splits(dt, 1, 32, 7, 512, 512, 3, 1) == 1
+    # small grids (batch 1-2, <= 64 64x64 tiles) with >= 16 K-steps: four splits (round 6)
+    for dt in (DT_BF16, DT_F32):
+        assert splits(dt, 0, 1, 7, 512, 512, 3, 1) == 4       # layer4 3x3 at B = 1: 8 tiles
+        assert splits(dt, 0, 1, 14, 1024, 256, 1, 1) == 4     # 16 K-steps (bf16), 16 tiles
+        assert splits(dt, 0, 1, 7, 512, 2048, 1, 1) == (1 if dt == DT_BF16 else 4)   # 8 (bf16) / 16 (fp32) K-steps
+        assert splits(dt, 0, 2, 14, 256, 256, 3, 1) == 4      # B = 2: 32 tiles
+        assert splits(dt, 0, 32, 7, 512, 512, 3, 1) == 2      # batch 32 unchanged
 
     # the split-K workspace a plan needs (caller-provided: 32 KiB of counters + partial tiles)
     def ws(dt, pas, N, H, Cin, Cout, k, s):
@@ -80,3 +87,19 @@ def test_dual_eval_launch_rejects_split_k_geometry():
                                         ctypes.c_void_p(1), 1, None)
     assert rc == 1
     assert b"split K" in lib.pose6d_last_error()
+
+
+def test_add_eval_table_arguments_checked_without_gpu():
+    """pose6d_add_neighbors / pose6d_add_eval_nbr refuse a neighbour count other than 8 / 16 / 32,
+    meshes beyond the uint16 index range and a misaligned table, before any launch."""
+    lib = _lib.load()
+    one = ctypes.c_void_p(16)
+    rc = lib.pose6d_add_neighbors(one, one, one, 1, 100, 12, one, None)
+    assert rc == 1 and b"K must be 8, 16 or 32" in lib.pose6d_last_error()
+    rc = lib.pose6d_add_neighbors(one, one, one, 1, 70000, 16, one, None)
+    assert rc == 1 and b"bad table sizes" in lib.pose6d_last_error()
+    args = [one] * 5 + [1] + [one] * 5 + [1, 100]
+    rc = lib.pose6d_add_eval_nbr(*args, ctypes.c_void_p(24), 16, *([one] * 7), None)   # 8-byte aligned table
+    assert rc == 1 and b"16-byte alignment" in lib.pose6d_last_error()
+    rc = lib.pose6d_add_eval_nbr(*args, one, 24, *([one] * 7), None)
+    assert rc == 1 and b"K in {8, 16, 32}" in lib.pose6d_last_error()
