@@ -1550,6 +1550,11 @@ bool fast_ok(int dtype, int mode, const Geom& g) {
 #endif
 int pick_tile_fast(int dtype, int64_t M, int N, int K) {
   const int64_t wg4 = p6::ceil_div(M, 128) * (int64_t)p6::ceil_div(N, 128);
+#ifndef POSE6D_F32_TILE_RULE
+#define POSE6D_F32_TILE_RULE 0   // build-time (A/B): 1 = 128x128 from K >= 256 on >= 96 tiles, 2 = from K >= 128, N >= 128
+#endif
+  if (dtype == POSE6D_DT_F32 && POSE6D_F32_TILE_RULE == 1) return (K >= 256 && N >= 128 && wg4 >= 96) ? 4 : 3;
+  if (dtype == POSE6D_DT_F32 && POSE6D_F32_TILE_RULE == 2) return (K >= 128 && N >= 128) ? 4 : 3;
   if (dtype == POSE6D_DT_F32) return (K >= 512 && N >= 128 && wg4 >= 192 && wg4 < 384) ? 4 : 3;
   return (N >= 128 && K >= POSE6D_TILE4_MIN_K && wg4 >= 384) ? 4 : 3;
 }
