@@ -43,7 +43,7 @@ ADD_FLOPS_PER_PAIR = 8.0       # 3 sub, 1 mul, 2 fma per ADD-S p
 # WRITE_SIZE / SQ_VALU_MFMA_BUSY_CYCLES runs, FETCH_SIZE doubled for gfx950) the roofline
 # `traffic` field is read from: one explicit file per compute dtype, updated in the commit
 # that adds a newer pass (never picked by file-name order).  --pmc-bf16 / --pmc-f32 override.
-PMC_SUMMARY = {"bf16": "profiles/r06g_pmc.json", "f32": "profiles/r06g_f32_pmc.json"}
+PMC_SUMMARY = {"bf16": "profiles/r06h_pmc.json", "f32": "profiles/r06h_f32_pmc.json"}
 
 
 def synth_batch(B, dev, seed):
