@@ -9,6 +9,8 @@ Linear -> BatchNorm1d -> ReLU -> Dropout runs as 2 launches (GEMM + fused
 BN/ReLU/dropout column kernel), Linear -> LayerNorm -> GELU -> Dropout as 2
 (GEMM + fused row kernel); buffers are preallocated per batch size.
 """
+import ctypes
+
 import torch
 import torch.nn as nn
 
@@ -176,7 +178,13 @@ class HeadEngine:
         self._saved_gen = -1 if skip >= 0 else self.generation   # fused: no backward state
         return cur
 
-    def backward(self, dy, grad_of, accumulate=False, need_dx=True):
+    def backward(self, dy, grad_of, accumulate=False, need_dx=True, wgrad_stream=None):
+        """wgrad_stream (a torch.cuda.Stream, optional): the Linear weight gradients,
+        which nothing downstream of the head's data gradient reads, run there -- each
+        after the current stream's work up to its launch -- so they overlap the trunk
+        backward; the caller joins it (current_stream().wait_stream) before anything
+        reads those gradients.  Their operands (the saved inputs, the stage gradients)
+        are persistent buffers, next written by the following step's forward."""
         if self._saved_gen != self.generation:
             raise Pose6dError("HeadEngine.backward without matching forward")
         st_ = stream()
@@ -190,8 +198,12 @@ class HeadEngine:
                 m = st.mod
                 K, N = m.in_features, m.out_features
                 # dW[N][K] = dy^T x and db = colsum(dy), one launch
+                ws_ = st_
+                if wgrad_stream is not None:
+                    wgrad_stream.wait_stream(torch.cuda.current_stream())
+                    ws_ = ctypes.c_void_p(wgrad_stream.cuda_stream)
                 call("linear_wgrad", g, N, st.x, K, grad_of(m.weight),
-                     grad_of(m.bias) if m.bias is not None else None, N, K, B, acc, st_)
+                     grad_of(m.bias) if m.bias is not None else None, N, K, B, acc, ws_)
                 if last and not need_dx:
                     return None
                 call("gemm_f32", g, N, 1, m.weight.detach(), K, 1, st.dx, K, None, B, K, N, 1.0, 0.0, self.ws,

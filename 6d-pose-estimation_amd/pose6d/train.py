@@ -30,6 +30,7 @@ MI355X design:
     per step instead of ~300 eager launches).
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -40,6 +41,11 @@ from .head import HeadEngine
 from .trunk import TrunkEngine
 
 NPART = 1024
+# POSE6D_HEAD_WGRAD_SIDE=1: the head's Linear weight gradients on a side stream in the
+# one-GPU step (step_body) -- bit-identical, but the replayed graph with that one parallel
+# branch measured 0.35 ms SLOWER per step (bf16 4.48 -> 4.84 ms, fp32 11.58 -> 11.90 ms,
+# profiles/r06h_head_side_stream_rejected.txt): off, kept for A/B
+POSE6D_HEAD_WGRAD_SIDE = os.environ.get("POSE6D_HEAD_WGRAD_SIDE", "0") == "1"
 
 
 class FlatArena:
@@ -225,21 +231,34 @@ class RGBDGeometricTrainer:
         """One training step without graphs (reference order of operations)."""
         self._sync_if_stale()
         if not self._ddp:
-            return self.step_body(data)
+            return self.step_body(data, branch=True)
         self._pack()
         self._forward_loss(*data)
         dfeat = self._head_backward()
         self._backward_ddp(dfeat)
         self._optimizer()
 
-    def step_body(self, data):
+    def step_body(self, data, branch=False):
         """The one-GPU step's launches, in order (what capture() records for world == 1;
-        pose6d.steptime captures it for in-step kernel timing)."""
+        pose6d.steptime captures it for in-step kernel timing).  branch=True (the
+        captured and eager one-GPU step) with POSE6D_HEAD_WGRAD_SIDE=1 (off by default:
+        measured slower): the head's Linear weight gradients run on a side stream,
+        overlapping the trunk backward, joined before the optimizer reads the
+        gradients; otherwise the graph is one chain (pose6d.steptime splices its event
+        nodes into a chain)."""
         self._pack()
         self._forward_loss(*data)
-        dfeat = self._head_backward()
+        side = self._side_stream() if branch and POSE6D_HEAD_WGRAD_SIDE else None
+        dfeat = self.head.backward(self.draw, self.arena.grad_of, wgrad_stream=side)
         self.trunk.backward(dfeat, self.arena.grad_of)
+        if side is not None:
+            torch.cuda.current_stream().wait_stream(side)
         self._optimizer()
+
+    def _side_stream(self):
+        if not hasattr(self, "_side"):
+            self._side = torch.cuda.Stream(device=self.dev)
+        return self._side
 
     # ------------------------------------------------------------- DDP backward
     def _backward_ddp(self, dfeat):
@@ -278,7 +297,7 @@ class RGBDGeometricTrainer:
         if not self._ddp:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                self.step_body(data)
+                self.step_body(data, branch=True)
             self.graphs = [g]
         else:
             self.graphs = self._capture_segments(data)
