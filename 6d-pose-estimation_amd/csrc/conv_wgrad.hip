@@ -461,6 +461,13 @@ Plan plan(int dtype, int M, int Cout, int Kpad, int SC, const pose6d_tuning_t* t
   if (POSE6D_WGRAD_BF128_ONE_SPLIT_TILES > 0 && p.fast && dtype == POSE6D_DT_BF16 && p.bm == 128 &&
       tiles >= POSE6D_WGRAD_BF128_ONE_SPLIT_TILES)
     target = tiles;
+#ifndef POSE6D_WGRAD_NARROW1X1_TARGET
+#define POSE6D_WGRAD_NARROW1X1_TARGET 0   // build-time (A/B): target of the bf16 1x1 256 -> 64 weight gradients (layer1's
+                                          // residual-junction convs; 0 = the 1x1 target)
+#endif
+  if (POSE6D_WGRAD_NARROW1X1_TARGET > 0 && p.fast && dtype == POSE6D_DT_BF16 && Kpad == SC && Cout == 64 &&
+      Kpad >= 4 * Cout)
+    target = POSE6D_WGRAD_NARROW1X1_TARGET;
   // aim for ~`target` workgroups, each reducing >= min_rows pixels, slabs capped in bytes
   int splits = p6::ceil_div(target, tiles);
   const int max_splits = p6::ceil_div(M, min_rows);
